@@ -1,0 +1,263 @@
+"""Throughput benchmark of the picotron training step on MI355X (BASELINE.json metric:
+tokens/sec/GPU + MFU, SmolLM-1.7B seq1024 at DP=1/2/4/8).
+
+A step is the reference's training step (ref train.py:219-240): optimizer.zero_grad(), grad_acc
+micro-batches of forward + backward (DP bucket all-reduce on the last), optimizer.step(), model.reset().
+Workload: SmolLM-1.7B geometry, 15 layers, seq 1024, micro-batch 4, grad_acc 32 per GPU (the
+reference README / config 3 per-GPU workload; weak scaling over DP), bf16, random init with the
+reference's init procedure, synthetic uniform tokens already resident on the GPU.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--grad-acc G] [--no-cpu-baseline]
+For N > 1 the driver launches one process per GPU with torch.distributed.run; DP gradients are
+all-reduced over RCCL (xGMI) by DataParallelBucket.
+
+Rank 0 prints ONE JSON line with `value` = whole-job tokens/s, a `roofline` object for the
+dominant kernel (timed live with HIP events on its own launch stream) and a `cpu_baseline` object
+(the oracle's CPU restatement of the same step on a bounded sample, rank 0 at N=1 only).
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+SEQ, MBS, LAYERS = 1024, 4, 15
+HBM_PEAK_GBS = 8000.0
+BF16_PEAK_TFLOPS = 256 * 4096 * 2.4e9 / 1e12  # 2516.6 dense
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def kernel_work(kid, cfg, mbs, seq):
+    """Algorithmic work of ONE launch of kernel `kid` at this workload: (amount, unit, bound).
+    Bytes: every input read once + every output written once."""
+    from picotron_amd import _lib as L
+    T = mbs * seq
+    Hd, I, H = cfg.hidden_size, cfg.intermediate_size, cfg.num_attention_heads
+    D = Hd // H
+    attn_fwd = 4.0 * mbs * H * seq * seq * D / 2  # causal
+    table = {
+        L.K_ATTN_FWD: (attn_fwd, "flop", "mfma"),
+        L.K_ATTN_BWD: (2.5 * attn_fwd, "flop", "mfma"),
+        L.K_RMSNORM_FWD: (2 * T * Hd * 2 + 4 * T, "byte", "hbm"),
+        L.K_RMSNORM_BWD: (3 * T * Hd * 2 + 4 * T, "byte", "hbm"),
+        L.K_ROPE: (2 * T * Hd * 2, "byte", "hbm"),  # one of q / k per launch (Hq = Hkv)
+        L.K_SWIGLU_FWD: (3 * T * I * 2, "byte", "hbm"),
+        L.K_SWIGLU_BWD: (5 * T * I * 2, "byte", "hbm"),
+        L.K_ATTN_BWD_PRE: (2 * T * Hd * 2 + T * H * 4 + T * Hd * 4, "byte", "hbm"),
+        L.K_ATTN_BWD_DQ: (T * Hd * 4 + T * Hd * 2, "byte", "hbm"),
+    }
+    return table.get(kid)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--grad-acc", type=int, default=32)
+    ap.add_argument("--layers", type=int, default=LAYERS)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--cpu-seq", type=int, default=256)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+    torch.cuda.set_device(local_rank)
+    device = torch.device("cuda", local_rank)
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29561")
+    os.environ.setdefault("RANK", str(rank))
+    os.environ.setdefault("WORLD_SIZE", str(world))
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
+
+    from picotron_amd import _lib as L
+    from picotron_amd import process_group_manager as pgm
+    from picotron_amd.data import SyntheticDataLoader
+    from picotron_amd.data_parallel.data_parallel import DataParallelBucket
+    from picotron_amd.model import build_llama, smollm_1_7b
+    from picotron_amd.train import get_mfu, train_step
+
+    L.load()
+    pgm.setup_process_group_manager(tp_size=1, cp_size=1, pp_size=1, dp_size=world)
+    cfg = smollm_1_7b(num_hidden_layers=args.layers, seq_length=SEQ)
+    torch.manual_seed(42)  # ref train.py:103 (same seed on every rank: identical replicas)
+    t0 = time.time()
+    model = build_llama(cfg, device=device, dtype=torch.bfloat16)
+    num_params = sum(p.numel() for p in model.parameters())
+    if world > 1:
+        model = DataParallelBucket(model)
+    opt = torch.optim.AdamW(model.parameters(), lr=3e-4)  # ref train.py:209 (non-fused in practice)
+    loader = SyntheticDataLoader(MBS, SEQ, args.grad_acc, cfg.vocab_size, seed=1234, kind="uniform",
+                                 num_batches=args.grad_acc, device=device)
+    log(f"[rank {rank}] model {num_params / 1e9:.3f}B params built in {time.time() - t0:.1f}s")
+
+    def step():
+        opt.zero_grad()
+        loss = train_step(model, loader, device)
+        opt.step()
+        if hasattr(model, "reset"):
+            model.reset()
+        return loss
+
+    for i in range(args.warmup):
+        ts = time.time()
+        loss = step()
+        log(f"[rank {rank}] warmup {i}: loss {loss:.4f} ({time.time() - ts:.2f}s)")
+
+    kernel_ids = [L.K_ATTN_FWD, L.K_ATTN_BWD, L.K_ATTN_BWD_PRE, L.K_ATTN_BWD_DQ, L.K_RMSNORM_FWD, L.K_RMSNORM_BWD,
+                  L.K_RMSNORM_DW, L.K_ROPE, L.K_SWIGLU_FWD, L.K_SWIGLU_BWD, L.K_GRAD_ACCUM, L.K_CAST]
+    if not args.no_kernel_timing:
+        cap = args.steps * args.grad_acc * (args.layers * 4 + 8) + 16
+        for k in kernel_ids:
+            L.prof_enable(k, cap)
+
+    dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    losses = []
+    for i in range(args.steps):
+        losses.append(step())
+    torch.cuda.synchronize()
+    dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+
+    kernels = {}
+    if not args.no_kernel_timing:
+        for k in kernel_ids:
+            tot, n = L.prof_collect(k)
+            if n:
+                kernels[L.KERNEL_NAMES[k]] = {"total_ms": tot, "launches": n, "avg_us": 1e3 * tot / n}
+        L.load().pico_prof_enable(0, 0)
+
+    tokens = world * MBS * SEQ * args.grad_acc * args.steps
+    value = tokens / elapsed
+    tps_gpu = value / world
+    mfu = get_mfu(tps_gpu, num_params, cfg)
+    ms_per_step = 1e3 * elapsed / args.steps
+    log(f"[rank {rank}] Step time {ms_per_step:.1f} ms | Loss: {losses[-1]:6.4f} | Tokens/s: {value:,.0f} | "
+        f"Tokens/s/GPU: {tps_gpu:,.0f} | MFU: {mfu:5.2f}%")
+
+    roofline = None
+    if kernels:
+        # dominant kernel = most total time among those with a stated algorithmic work
+        cand = [(v["total_ms"], name) for name, v in kernels.items()
+                if kernel_work([k for k in kernel_ids if L.KERNEL_NAMES[k] == name][0], cfg, MBS, SEQ)]
+        _, dom = max(cand)
+        kid = [k for k in kernel_ids if L.KERNEL_NAMES[k] == dom][0]
+        amount, unit, bound = kernel_work(kid, cfg, MBS, SEQ)
+        avg_s = kernels[dom]["avg_us"] * 1e-6
+        if unit == "flop":
+            achieved, peak, u = amount / avg_s / 1e12, BF16_PEAK_TFLOPS, "TFLOP/s"
+        else:
+            achieved, peak, u = amount / avg_s / 1e9, HBM_PEAK_GBS, "GB/s"
+        roofline = {"kernel": dom, "bound": bound, "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": u,
+                    "frac": round(achieved / peak, 4), "traffic": None,
+                    "work_per_launch": amount, "avg_launch_us": round(kernels[dom]["avg_us"], 2)}
+        for name, v in kernels.items():
+            kk = [k for k in kernel_ids if L.KERNEL_NAMES[k] == name][0]
+            w = kernel_work(kk, cfg, MBS, SEQ)
+            if w:
+                a = w[0] / (v["avg_us"] * 1e-6)
+                v["achieved"] = round(a / 1e12, 2) if w[1] == "flop" else round(a / 1e9, 1)
+                v["unit"] = "TFLOP/s" if w[1] == "flop" else "GB/s"
+                v["frac"] = round(v["achieved"] / (BF16_PEAK_TFLOPS if w[1] == "flop" else HBM_PEAK_GBS), 4)
+            v["total_ms"] = round(v["total_ms"], 3)
+            v["avg_us"] = round(v["avg_us"], 2)
+
+    cpu_baseline = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu_baseline = run_cpu_baseline(cfg, model, args.cpu_seq)
+
+    if rank == 0:
+        out = {
+            "metric": "tokens/sec/GPU + MFU, SmolLM-1.7B seq1024",
+            "value": round(value, 1),
+            "unit": "tokens/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 2),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (uniform token ids, reference random init)",
+            "config": {"workload": "SmolLM-1.7B 15 layers, seq 1024, micro-batch 4, grad_acc %d per GPU, "
+                                   "full training step (fwd+bwd+AdamW)" % args.grad_acc,
+                       "model": "SmolLM-1.7B-%dL" % args.layers, "global_batch": MBS * args.grad_acc * world,
+                       "seq_len": SEQ, "micro_batch": MBS, "grad_acc": args.grad_acc, "parallelism": f"dp{world}"},
+            "tokens_per_sec_per_gpu": round(tps_gpu, 1),
+            "mfu_pct": round(mfu, 2),
+            "mfu_peak_tflops": round(BF16_PEAK_TFLOPS, 1),
+            "num_params": num_params,
+            "loss_last": round(losses[-1], 4),
+            "roofline": roofline,
+            "kernels": kernels,
+            "cpu_baseline": cpu_baseline,
+        }
+        print(json.dumps(out), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def run_cpu_baseline(cfg, gpu_model, seq):
+    """Oracle (CPU restatement of the reference's eager fp32 path, oracle/model.py) timed on this
+    host's cores on a bounded sample of the same step: the full 15-layer SmolLM-1.7B, one micro-batch
+    of 1 x `seq` tokens, forward + backward + AdamW."""
+    from oracle import model as OM
+    ncores = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    torch.set_num_threads(ncores)
+    from types import SimpleNamespace
+    ocfg = SimpleNamespace(**{**cfg.__dict__, "max_position_embeddings": seq})
+    with torch.device("meta"):
+        m = OM.Llama(ocfg)
+    m.to_empty(device="cpu")
+    from oracle import hotpath as H
+    D = cfg.hidden_size // cfg.num_attention_heads
+    for layer in m.decoder_layers:
+        layer.cos, layer.sin = H.get_cos_sin(seq, D, cfg.rope_theta)
+    src = dict(gpu_model.named_parameters())
+    with torch.no_grad():  # same weights as the GPU model (fp32), no CPU RNG init cost
+        for n, p in m.named_parameters():
+            key = n if n in src else "module." + n
+            p.copy_(src[key].detach().float().cpu())
+    opt = torch.optim.AdamW(m.parameters(), lr=3e-4)
+    gen = torch.Generator().manual_seed(0)
+    toks = torch.randint(0, cfg.vocab_size, (1, seq + 1), generator=gen)
+    batch = [(toks[:, :-1], toks[:, 1:])]
+    OM.train_step(m, batch, 1)  # warm-up (allocations)
+    opt.zero_grad()
+    t0 = time.perf_counter()
+    n = 0
+    while True:
+        OM.train_step(m, batch, 1)
+        opt.step()
+        opt.zero_grad()
+        n += 1
+        if time.perf_counter() - t0 > 10.0 or n >= 3:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": round(n * seq / dt, 2), "unit": "tokens/s", "cores": ncores, "kind": "port",
+            "sample": f"{n} x full step (fwd+bwd+AdamW) of SmolLM-1.7B-15L fp32 eager (oracle/model.py), "
+                      f"micro-batch 1x{seq} tokens, {dt:.1f}s"}
+
+
+if __name__ == "__main__":
+    main()

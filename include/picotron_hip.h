@@ -1,0 +1,150 @@
+/*
+ * picotron_hip.h — C ABI of the MI355X (gfx950) hot-path kernels of picotron_amd.
+ *
+ * The reference (rkinas/picotron) is pure Python; its native arithmetic lives in
+ * flash-attn 2.5.0 (CUDA + Triton) and torch ATen/NCCL. Each entry point below replaces one
+ * of those third-party calls made from the reference's model / data-parallel code:
+ *
+ *   pico_rmsnorm_fwd / _bwd   <- flash_attn.ops.triton.layer_norm.layer_norm_fn(is_rms_norm=True)
+ *                                 called by TritonRMSNorm.forward   (ref picotron/model.py:50-64)
+ *                                 eager oracle LlamaRMSNorm          (ref picotron/model.py:66-85)
+ *   pico_rope                 <- flash_attn.layers.rotary.apply_rotary_emb(x, cos, sin, interleaved=False)
+ *                                 called by Attention.forward         (ref picotron/model.py:135-136)
+ *                                 (conjugate=1 is its backward: rotation by -theta)
+ *   pico_swiglu_fwd / _bwd    <- F.silu(gate(x)) * up(x)             (ref picotron/model.py:185)
+ *   pico_attn_fwd / _bwd      <- flash_attn_func(q, k, v, causal)     (ref picotron/model.py:32-36,153)
+ *                                 and the ring-attention block fwd/bwd
+ *                                 (ref picotron/context_parallel/context_parallel.py:112-155)
+ *   pico_attn_merge           <- update_out_and_lse                  (ref .../context_parallel.py:157-187)
+ *   pico_grad_accum           <- param.main_grad.add_(param.grad)    (ref picotron/data_parallel/data_parallel.py:131)
+ *                                 fused with Bucket.sync_gradient's grad_data /= W
+ *                                                                      (ref picotron/data_parallel/bucket.py:30)
+ *   pico_cast_f32_bf16        <- p.grad = p.main_grad.to(p.dtype)    (ref picotron/data_parallel/data_parallel.py:165)
+ *   pico_scale_f32            <- grad_data /= process_group_size     (ref picotron/data_parallel/bucket.py:30)
+ *
+ * Conventions: all pointers are device pointers allocated by the caller (kernels never
+ * allocate); bf16 tensors are passed as raw 16-bit storage; `stream` is a hipStream_t
+ * (the caller's current stream). Every function returns 0 on success or a non-zero
+ * status (hipError_t value, or PICO_EINVAL for argument errors); pico_last_error()
+ * returns the message for the calling thread. No C++ exception crosses the ABI.
+ */
+#ifndef PICOTRON_HIP_H
+#define PICOTRON_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PICO_ABI_VERSION 1
+#define PICO_EINVAL 1000
+
+/* kernel ids for the optional event timer (pico_prof_*) */
+enum {
+  PICO_K_RMSNORM_FWD = 1,
+  PICO_K_RMSNORM_BWD = 2,
+  PICO_K_RMSNORM_DW = 3,
+  PICO_K_ROPE = 4,
+  PICO_K_SWIGLU_FWD = 5,
+  PICO_K_SWIGLU_BWD = 6,
+  PICO_K_ATTN_FWD = 7,
+  PICO_K_ATTN_BWD_PRE = 8,
+  PICO_K_ATTN_BWD = 9,
+  PICO_K_ATTN_BWD_DQ = 10,
+  PICO_K_GRAD_ACCUM = 11,
+  PICO_K_CAST = 12,
+  PICO_K_SCALE = 13,
+  PICO_K_ATTN_MERGE = 14,
+  PICO_K_COUNT = 15
+};
+
+int pico_abi_version(void);
+const char* pico_last_error(void);
+
+/* ---- event timer: times every launch of the enabled kernel ids on the stream each is launched on ----
+ * pico_prof_enable(id, capacity) enables id (up to `capacity` timed launches); id <= 0 disables all.
+ * pico_prof_collect(id, ...) synchronises the recorded events, returns their summed duration and
+ * count, and resets that id's pool. */
+int pico_prof_enable(int kernel_id, int capacity);
+int pico_prof_collect(int kernel_id, double* total_ms, int64_t* launches);
+
+/* ---- RMSNorm: y = x * rsqrt(mean(x^2) + eps) * w, fp32 math, one bf16 rounding ----
+ * x, y: [rows, cols] bf16 row-major (row stride = cols); w: [cols] bf16; rstd: [rows] fp32 (saved
+ * for backward). residual (optional, may be NULL): x_eff = bf16(x + residual), written to
+ * residual_out when residual_out != NULL (layer_norm_fn(prenorm=True) semantics). */
+int pico_rmsnorm_fwd(const void* x, const void* residual, const void* weight, void* y,
+                     void* residual_out, float* rstd, int64_t rows, int64_t cols, float eps,
+                     void* stream);
+int64_t pico_rmsnorm_bwd_workspace_bytes(int64_t rows, int64_t cols);
+/* dx: [rows, cols] bf16; dweight: [cols] bf16; workspace >= pico_rmsnorm_bwd_workspace_bytes.
+ * dresidual (optional, may be NULL): added into dx (gradient flowing through residual_out). */
+int pico_rmsnorm_bwd(const void* dy, const void* dresidual, const void* x, const void* weight,
+                     const float* rstd, void* dx, void* dweight, void* workspace, int64_t rows,
+                     int64_t cols, void* stream);
+
+/* ---- RoPE, rotate-half (non-interleaved) layout ----
+ * x, out: [batch, seqlen, heads, head_dim] bf16 with element strides (batch, seq, head) and
+ * unit last-dim stride (out may alias x). cos/sin: [seqlen, >= head_dim/2] bf16 tables with
+ * row stride cs_stride (elements); element i < head_dim/2 of row s is cos(s * theta_i).
+ * out[..., i]       = x[i] * c - x[i + D/2] * s
+ * out[..., i + D/2] = x[i + D/2] * c + x[i] * s        (conjugate: s -> -s, the backward) */
+int pico_rope(const void* x, void* out, const void* cos, const void* sin, int64_t batch,
+              int64_t seqlen, int64_t heads, int64_t head_dim, const int64_t* x_strides,
+              const int64_t* out_strides, int64_t cs_stride, int conjugate, void* stream);
+
+/* ---- SwiGLU epilogue: h = silu(g) * u over n contiguous bf16 elements ---- */
+int pico_swiglu_fwd(const void* gate, const void* up, void* out, int64_t n, void* stream);
+int pico_swiglu_bwd(const void* dout, const void* gate, const void* up, void* dgate, void* dup,
+                    int64_t n, void* stream);
+
+/* ---- Flash attention (bf16 MFMA, online softmax, fp32 LSE) ----
+ * Layouts: q/o/do/dq [B, Sq, Hq, D], k/v/dk/dv [B, Sk, Hkv, D] with element strides
+ * (batch, seq, head) and unit last-dim stride; lse [B, Hq, Sq] fp32 contiguous (natural log,
+ * lse = log sum_j exp(scale * q.k_j)). Hq % Hkv == 0 (GQA: query head h uses kv head h/(Hq/Hkv)).
+ * head_dim in {64, 128}. causal requires Sq == Sk (top-left aligned mask j <= i). */
+typedef struct pico_attn_args {
+  const void* q;
+  const void* k;
+  const void* v;
+  void* o;          /* fwd output / bwd input */
+  float* lse;       /* fwd output / bwd input */
+  const void* dout; /* bwd */
+  void* dq;         /* bwd out (bf16, or fp32 accumulate with PICO_ATTN_DQ_F32_ACCUM) */
+  void* dk;         /* bwd out bf16 */
+  void* dv;         /* bwd out bf16 */
+  void* workspace;  /* bwd: >= pico_attn_bwd_workspace_bytes */
+  int64_t batch, seqlen_q, seqlen_k, heads_q, heads_kv, head_dim;
+  int64_t q_strides[3], k_strides[3], v_strides[3], o_strides[3];
+  int64_t do_strides[3], dq_strides[3], dk_strides[3], dv_strides[3];
+  float softmax_scale;
+  int causal;
+  int flags;
+} pico_attn_args;
+
+#define PICO_ATTN_DQ_F32_ACCUM 1 /* dq is fp32 [B,Sq,Hq,D] (dq_strides) and is ADDED into */
+
+int64_t pico_attn_args_size(void); /* sizeof(pico_attn_args), for FFI layout checks */
+int pico_attn_fwd(const pico_attn_args* args, void* stream);
+int64_t pico_attn_bwd_workspace_bytes(const pico_attn_args* args);
+int pico_attn_bwd(const pico_attn_args* args, void* stream);
+
+/* ---- ring-attention block merge (update_out_and_lse) ----
+ * out fp32 [B, S, H, D] contiguous, lse fp32 [B, H, S]; block_out bf16 [B, S, H, D] with element
+ * strides (batch, seq, head); block_lse fp32 [B, H, S]. first != 0: out = block_out, lse = block_lse. */
+int pico_attn_merge(float* out, float* lse, const void* block_out, const float* block_lse, int64_t batch,
+                    int64_t seqlen, int64_t heads, int64_t head_dim, const int64_t* block_out_strides, int first,
+                    void* stream);
+
+/* ---- DP gradient buckets ---- */
+/* main_grad[i] = (main_grad[i] + float(grad[i])) / divide_by   (divide_by == 1: no division) */
+int pico_grad_accum(float* main_grad, const void* grad, int64_t n, float divide_by, void* stream);
+/* buf[i] = buf[i] / divide_by */
+int pico_scale_f32(float* buf, int64_t n, float divide_by, void* stream);
+/* dst[i] = bf16(src[i]) (round to nearest even) */
+int pico_cast_f32_bf16(const float* src, void* dst, int64_t n, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PICOTRON_HIP_H */

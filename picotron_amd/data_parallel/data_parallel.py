@@ -1,0 +1,115 @@
+"""Data-parallel wrappers — same API as the reference picotron/data_parallel/data_parallel.py:
+DataParallelNaive (:10-60) and DataParallelBucket (:62-171).
+
+DataParallelBucket keeps the reference's contract (attributes `.module`,
+`.require_backward_grad_sync`, `.bucket_manager`; `forward`, `backward(input, output, output_grad)`
+for pipeline parallelism, `no_sync()`, `reset()`; fp32 `param.main_grad` views; after a syncing
+backward every param's `.grad` holds the bf16 average). Per-parameter post-accumulate hooks
+(the reference hooks the AccumulateGrad node, ref :93-116; torch's
+register_post_accumulate_grad_hook is the same event) run on the autograd device thread:
+  * `main_grad += grad` on the pico_grad_accum kernel, fused with the 1/W pre-scale when syncing;
+  * when a bucket's last param arrives, its RCCL all-reduce is launched asynchronously and its
+    bf16 cast is queued behind it on a side stream (see bucket.py);
+  * the post-backward callback makes the compute stream wait for every bucket and hands out the
+    `.grad` views.
+"""
+import contextlib
+
+import torch
+import torch.distributed as dist
+from torch import nn
+from torch.autograd import Variable
+
+from .. import process_group_manager as pgm
+from .bucket import BucketManager
+
+
+class DataParallelNaive(nn.Module):
+    """Per-gradient all-reduce (ref :10-60; kept for API completeness, unused by the trainer)."""
+
+    def __init__(self, module):
+        super().__init__()
+        self.module = module
+        self.require_backward_grad_sync = True
+        self.register_backward_hook(self._allreduce_grads)
+
+    def forward(self, *inputs, **kwargs):
+        return self.module(*inputs, **kwargs)
+
+    def register_backward_hook(self, hook):
+        for p in self.module.parameters():
+            if p.requires_grad is True:
+                p.register_hook(hook)
+
+    def _allreduce_grads(self, grad):
+        if self.require_backward_grad_sync:
+            dist.all_reduce(grad, op=dist.ReduceOp.SUM, group=pgm.process_group_manager.cp_dp_group)
+            grad /= pgm.process_group_manager.cp_dp_world_size
+        return grad
+
+    @contextlib.contextmanager
+    def no_sync(self):
+        self.require_backward_grad_sync = False
+        yield
+        self.require_backward_grad_sync = True
+
+
+class DataParallelBucket(nn.Module):
+
+    def __init__(self, module, bucket_cap_mb=25, grad_type=torch.float32):
+        super().__init__()
+        self.module = module
+        self.require_backward_grad_sync = True
+        grad_size = 2 if grad_type == torch.bfloat16 else 4
+        bucket_size = bucket_cap_mb * 1024 * 1024 // grad_size
+        self.bucket_manager = BucketManager(module.parameters(), pgm.process_group_manager.cp_dp_group, bucket_size,
+                                            grad_type)
+        self.register_backward_hook()
+        self._post_backward_callback_set = False
+
+    def forward(self, *inputs, **kwargs):
+        return self.module(*inputs, **kwargs)
+
+    def backward(self, input_tensor, output_tensor, output_tensor_grad):
+        return self.module.backward(input_tensor, output_tensor, output_tensor_grad)
+
+    def register_backward_hook(self):
+        self.grad_accs = []
+        for param in self.module.parameters():
+            if param.requires_grad:
+                self.grad_accs.append(param.register_post_accumulate_grad_hook(
+                    self._make_param_hook(param, self.bucket_manager)))
+
+    def _make_param_hook(self, param, bucket_manager):
+        from .bucket import get_kernels
+        world = bucket_manager.process_group_size
+
+        def param_hook(*unused):
+            if param.requires_grad:
+                assert param.grad is not None
+                sync = self.require_backward_grad_sync
+                # fold the bucket's 1/W pre-scale into this (final) accumulate when syncing
+                get_kernels().accumulate(param.main_grad, param.grad, world if sync else 1)
+                param.grad = None
+                if sync:
+                    if not self._post_backward_callback_set:
+                        Variable._execution_engine.queue_callback(self._post_backward)
+                        self._post_backward_callback_set = True
+                    bucket_manager.mark_param_as_ready(param, prescaled=True)
+        return param_hook
+
+    @contextlib.contextmanager
+    def no_sync(self):
+        self.require_backward_grad_sync = False
+        yield
+        self.require_backward_grad_sync = True
+
+    def _post_backward(self):
+        self.bucket_manager.wait()
+        self._post_backward_callback_set = False
+        for p in self.module.parameters():
+            if p.requires_grad:
+                p.grad = self.bucket_manager.grad_view(p)
+
+    def reset(self):
+        self.bucket_manager.reset()

@@ -1,0 +1,275 @@
+"""Llama model whose hot path runs on the gfx950 kernels — same module API as the reference
+picotron/model.py (class names, constructor arguments, attribute names, parameter registration
+order and reset_parameters semantics), so tensor/pipeline/context-parallel wrappers that replace
+submodules by attribute name, and the DP bucket layout (which follows parameter order), see the
+same model.
+
+Hot-path mapping (reference -> here):
+  TritonRMSNorm / LlamaRMSNorm (ref :38-85)       -> RMSNorm on pico_rmsnorm_fwd/_bwd
+  apply_rotary_emb (ref :135-136)                 -> ops.apply_rotary_emb on pico_rope
+  flash_attn_func / SDPA (ref :153-156)           -> ops.flash_attn_func on pico_attn_fwd/_bwd (native
+                                                      GQA: no repeat_interleave copies, ref :141-142)
+  ring_attention (ref :147-150)                   -> context_parallel.ring_attention on the same kernels
+  F.silu(gate) * up (ref :185)                    -> ops.swiglu on pico_swiglu_fwd/_bwd
+There is no eager/CPU fallback: modules raise if the HIP library or a HIP device is missing.
+The GEMMs (q/k/v/out/up/gate/down/final projections) stay torch (hipBLASLt).
+"""
+import math
+import os
+from dataclasses import dataclass
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import ops
+from . import process_group_manager as pgm
+
+
+@dataclass
+class LlamaConfig:
+    """Geometry of a Llama model (the fields picotron reads from HF AutoConfig, ref train.py:152-165)."""
+    hidden_size: int = 2048
+    intermediate_size: int = 8192
+    num_attention_heads: int = 32
+    num_key_value_heads: int = 32
+    num_hidden_layers: int = 24
+    vocab_size: int = 49152
+    max_position_embeddings: int = 2048
+    rms_norm_eps: float = 1e-5
+    rope_theta: float = 10000.0
+
+
+def smollm_1_7b(num_hidden_layers=24, seq_length=2048):
+    """HuggingFaceTB/SmolLM-1.7B geometry (restated; checkpoints are not available offline)."""
+    return LlamaConfig(hidden_size=2048, intermediate_size=8192, num_attention_heads=32, num_key_value_heads=32,
+                       num_hidden_layers=num_hidden_layers, vocab_size=49152, max_position_embeddings=seq_length,
+                       rms_norm_eps=1e-5, rope_theta=10000.0)
+
+
+def llama2_7b(num_hidden_layers=32, seq_length=4096):
+    """meta-llama/Llama-2-7b-hf geometry (restated)."""
+    return LlamaConfig(hidden_size=4096, intermediate_size=11008, num_attention_heads=32, num_key_value_heads=32,
+                       num_hidden_layers=num_hidden_layers, vocab_size=32000, max_position_embeddings=seq_length,
+                       rms_norm_eps=1e-5, rope_theta=10000.0)
+
+
+def _table_device():
+    if os.getenv("DEVICE", "cuda") == "cuda" and torch.cuda.is_available():
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
+def get_cos_sin(seq_length, head_dim, base=500000.0):
+    """RoPE tables [seq_length, head_dim] (freqs repeated twice), ref picotron/model.py:21-30:
+    theta on CPU in fp32, position * theta and cos/sin on DEVICE, cast to DTYPE (bf16 default)."""
+    assert head_dim % 2 == 0
+    theta = 1.0 / (base ** (torch.arange(0, head_dim, 2, dtype=torch.int64, device="cpu").float() / head_dim))
+    dtype = torch.bfloat16 if os.getenv("DTYPE", "bfloat16") == "bfloat16" else torch.float32
+    device = _table_device()
+    position = torch.arange(seq_length, device="cpu").to(device).unsqueeze(1).float()
+    theta = theta.to(device)
+    ang = position.float() * theta.float()
+    return torch.cos(ang).to(dtype).repeat(1, 2), torch.sin(ang).to(dtype).repeat(1, 2)
+
+
+def apply_rotary_pos_emb(x, cos, sin):
+    """Rotate-half RoPE on x [B, H, S, D] with tables [S, D] (ref picotron/model.py:12-19), on the kernel."""
+    S, D = x.shape[2], x.shape[3]
+    out = ops.apply_rotary_emb(x.transpose(1, 2), cos[:S, : D // 2], sin[:S, : D // 2])
+    return out.transpose(1, 2)
+
+
+def flash_attention(q, k, v, causal=True):
+    """q, k, v [B, H, S, D] -> [B, S, H, D] (ref picotron/model.py:32-36)."""
+    return ops.flash_attn_func(q.permute(0, 2, 1, 3), k.permute(0, 2, 1, 3), v.permute(0, 2, 1, 3), causal=causal)
+
+
+class RMSNorm(nn.Module):
+    """Fused RMSNorm (ref TritonRMSNorm, picotron/model.py:38-64): same constructor, weight init
+    (ones) and forward signature; `residual`/`prenorm` fuse the residual add into the kernel."""
+
+    def __init__(self, hidden_size, eps=1e-5, device=None, dtype=None):
+        super().__init__()
+        self.eps = eps
+        self.variance_epsilon = eps  # LlamaRMSNorm attribute name (ref :73)
+        self.weight = nn.Parameter(torch.empty(hidden_size, device=device, dtype=dtype))
+        self.register_parameter("bias", None)
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        nn.init.ones_(self.weight)
+
+    def forward(self, hidden_states, residual=None, dropout_p=0.0, prenorm=False, residual_in_fp32=False,
+                return_dropout_mask=False):
+        return ops.layer_norm_fn(hidden_states, self.weight, None, residual=residual, eps=self.eps,
+                                 dropout_p=dropout_p, prenorm=prenorm, residual_in_fp32=residual_in_fp32,
+                                 is_rms_norm=True, return_dropout_mask=return_dropout_mask)
+
+
+TritonRMSNorm = RMSNorm
+LlamaRMSNorm = RMSNorm
+
+
+class Attention(nn.Module):
+    """ref picotron/model.py:87-161. q/k/v/out projections keep their names so TP can replace them."""
+
+    def __init__(self, config, layer_idx):
+        super().__init__()
+        tp = pgm.tp_world_size()
+        self.hidden_size = config.hidden_size
+        self.num_heads = config.num_attention_heads
+        self.num_key_values = config.num_key_value_heads
+        self.head_dim = self.hidden_size // self.num_heads
+        assert config.num_attention_heads % tp == 0, "num_attention_heads should be divisible by tp world size"
+        assert config.num_key_value_heads % tp == 0, "num_key_value_heads should be divisible by tp world size"
+        self.num_local_heads = config.num_attention_heads // tp
+        self.num_local_kv_heads = config.num_key_value_heads // tp
+        self.q_proj = nn.Linear(config.hidden_size, self.num_heads * self.head_dim, bias=False)
+        self.k_proj = nn.Linear(config.hidden_size, self.num_key_values * self.head_dim, bias=False)
+        self.v_proj = nn.Linear(config.hidden_size, self.num_key_values * self.head_dim, bias=False)
+        self.out_proj = nn.Linear(config.hidden_size, config.hidden_size, bias=False)
+        self.layer_idx = layer_idx
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        for w in (self.q_proj.weight, self.k_proj.weight, self.v_proj.weight, self.out_proj.weight):
+            bound = math.sqrt(1 / w.size(1))
+            torch.nn.init.uniform_(w, -bound, bound)
+
+    def forward(self, x, cos, sin, attention_mask=None, position_ids=None):
+        B, S, _ = x.size()
+        D = self.head_dim
+        q = self.q_proj(x).view(B, S, self.num_local_heads, D)
+        k = self.k_proj(x).view(B, S, self.num_local_kv_heads, D)
+        v = self.v_proj(x).view(B, S, self.num_local_kv_heads, D)
+        q = ops.apply_rotary_emb(q, cos[:, : D // 2], sin[:, : D // 2])
+        k = ops.apply_rotary_emb(k, cos[:, : D // 2], sin[:, : D // 2])
+        causal = q.size(1) == k.size(1)
+        if os.getenv("CONTEXT_PARALLEL", "0") == "1":
+            from .context_parallel import context_parallel
+            out = context_parallel.ring_attention(q, k, v, 1.0 / math.sqrt(D), causal)
+        else:
+            out = ops.flash_attn_func(q, k, v, causal=causal)
+        out = out.reshape(B, S, self.num_local_heads * D)
+        return self.out_proj(out)
+
+
+class MLP(nn.Module):
+    """ref picotron/model.py:163-185."""
+
+    def __init__(self, config) -> None:
+        super().__init__()
+        self.up_proj = nn.Linear(config.hidden_size, config.intermediate_size, bias=False)
+        self.gate_proj = nn.Linear(config.hidden_size, config.intermediate_size, bias=False)
+        self.down_proj = nn.Linear(config.intermediate_size, config.hidden_size, bias=False)
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        for w in (self.up_proj.weight, self.gate_proj.weight, self.down_proj.weight):
+            bound = math.sqrt(1 / w.size(1))
+            torch.nn.init.uniform_(w, -bound, bound)
+
+    def forward(self, x):
+        return self.down_proj(ops.swiglu(self.gate_proj(x), self.up_proj(x)))
+
+
+class DecoderLayer(nn.Module):
+    """RMSNorm -> Attention -> Residual -> RMSNorm -> MLP -> Residual (ref picotron/model.py:187-208)."""
+
+    def __init__(self, config, layer_idx):
+        super().__init__()
+        self.input_layernorm = RMSNorm(config.hidden_size, eps=config.rms_norm_eps)
+        self.post_attention_layernorm = RMSNorm(config.hidden_size, eps=config.rms_norm_eps)
+        self.attention = Attention(config, layer_idx=layer_idx)
+        self.mlp = MLP(config)
+        self.layer_idx = layer_idx
+        head_dim = config.hidden_size // config.num_attention_heads
+        cos, sin = get_cos_sin(config.max_position_embeddings, head_dim=head_dim, base=config.rope_theta)
+        from .context_parallel.context_parallel import update_rope_for_context_parallel
+        self.cos, self.sin = update_rope_for_context_parallel(cos, sin)
+
+    def forward(self, x, attention_mask=None, position_ids=None):
+        cos, sin = self.cos, self.sin
+        x = x + self.attention(self.input_layernorm(x), cos, sin, attention_mask, position_ids)
+        x = x + self.mlp(self.post_attention_layernorm(x))
+        return x
+
+
+class Embedding(nn.Module):
+    """ref picotron/model.py:210-224."""
+
+    def __init__(self, num_embeddings, embedding_dim, padding_idx=None):
+        super().__init__()
+        self.num_embeddings = num_embeddings
+        self.embedding_dim = embedding_dim
+        self.padding_idx = padding_idx
+        self.weight = nn.Parameter(torch.empty(num_embeddings, embedding_dim))
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        torch.nn.init.normal_(self.weight, mean=0.0, std=1.0)
+
+    def forward(self, x):
+        return F.embedding(x, self.weight, self.padding_idx)
+
+
+class Llama(nn.Module):
+    """ref picotron/model.py:226-271 (parameter order: embedding, layers (input_ln, post_attn_ln,
+    q, k, v, out, up, gate, down), final_proj, final_norm)."""
+
+    def __init__(self, config) -> None:
+        super().__init__()
+        assert config.hidden_size % config.num_attention_heads == 0
+        assert config.num_attention_heads % config.num_key_value_heads == 0
+        self.vocab_size = config.vocab_size
+        self.hidden_size = config.hidden_size
+        self.num_heads = config.num_attention_heads
+        self.num_key_values = config.num_key_value_heads
+        self.head_dim = self.hidden_size // self.num_heads
+        self.max_position_embeddings = config.max_position_embeddings
+        self.num_layers = config.num_hidden_layers
+        self.model_config = config
+        self.embedding = Embedding(self.vocab_size, self.hidden_size)
+        self.decoder_layers = nn.ModuleList([DecoderLayer(config, layer_idx=i) for i in range(self.num_layers)])
+        self.final_proj = nn.Linear(self.hidden_size, self.vocab_size, bias=False)
+        self.final_norm = RMSNorm(self.hidden_size, eps=config.rms_norm_eps)
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        self.embedding.reset_parameters()
+        for layer in self.decoder_layers:
+            layer.input_layernorm.reset_parameters()
+            layer.attention.reset_parameters()
+            layer.post_attention_layernorm.reset_parameters()
+            layer.mlp.reset_parameters()
+        self.final_norm.reset_parameters()
+        # NB: the reference never re-initialises final_proj here (ref :262 lacks the call); it is
+        # zero-initialised by init_model_with_materialized_weights (ref picotron/checkpoint.py:88-91).
+
+    def forward(self, input_ids, attention_mask=None, position_ids: torch.Tensor = None):
+        x = self.embedding(input_ids)
+        for layer in self.decoder_layers:
+            x = layer(x)
+        x = self.final_norm(x)
+        return self.final_proj(x)
+
+
+def build_llama(config, device="cuda", dtype=torch.bfloat16):
+    """Materialise a Llama exactly as the reference's non-PP init path does
+    (ref train.py:174-190, picotron/checkpoint.py:50-102): modules built without consuming RNG, params
+    materialised in fp32 on CPU, a fresh CPU nn.Linear LM head (kaiming draw) zero-filled, then
+    `reset_parameters()` draws from the CPU generator in module order (so set the seed first), then
+    cast to `dtype` and move to `device`."""
+    with torch.device("meta"):
+        model = Llama(config)
+    model.to_empty(device="cpu")
+    for p in model.parameters():
+        p.data = p.data.float()
+    # ref checkpoint.py:90: a fresh CPU nn.Linear for the LM head (its kaiming init draws from the
+    # CPU generator before reset_parameters), loaded with zeros (:91); registration order unchanged
+    model.final_proj = nn.Linear(config.hidden_size, config.vocab_size, bias=False)
+    with torch.no_grad():
+        model.final_proj.weight.zero_()
+    model.reset_parameters()
+    return model.to(dtype).to(device)

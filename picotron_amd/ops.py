@@ -1,0 +1,307 @@
+"""Hot-path ops on the gfx950 kernels, with the signatures of the third-party calls they replace.
+
+The reference imports three flash-attn entry points (ref picotron/model.py:7-9):
+    from flash_attn.flash_attn_interface import flash_attn_func
+    from flash_attn.layers.rotary import apply_rotary_emb
+    from flash_attn.ops.triton.layer_norm import layer_norm_fn
+This module exports functions of the same names and argument meanings, so the reference's own
+model.py runs on MI355X by swapping those three imports. Unsupported options
+(dropout, bias, interleaved rotary, windows, ...) raise NotImplementedError instead of silently
+doing something else, and every op raises if its inputs are not bf16 tensors on a HIP device.
+
+Extra entry points used by picotron_amd's own modules:
+    swiglu(gate, up)                          - F.silu(gate) * up      (ref picotron/model.py:185)
+    attention_block_fwd / attention_block_bwd - ring-attention block fwd/bwd with fp32 LSE
+                                                (ref picotron/context_parallel/context_parallel.py:112-155)
+"""
+import ctypes
+import math
+
+import torch
+
+from . import _lib
+
+_BF16 = torch.bfloat16
+
+
+def _need(t, name, dtype=_BF16):
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a tensor")
+    if t.device.type != "cuda":
+        raise RuntimeError(f"{name}: picotron_amd kernels need HIP tensors, got device {t.device}")
+    if dtype is not None and t.dtype != dtype:
+        raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
+
+
+# --------------------------------------------------------------------------------------------
+# RMSNorm  (flash_attn.ops.triton.layer_norm.layer_norm_fn with is_rms_norm=True)
+# --------------------------------------------------------------------------------------------
+class _RMSNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, residual, weight, eps, prenorm):
+        _need(x, "x")
+        _need(weight, "weight")
+        shape = x.shape
+        cols = shape[-1]
+        x2 = x.reshape(-1, cols).contiguous()
+        rows = x2.shape[0]
+        lib = _lib.load()
+        y = torch.empty_like(x2)
+        rstd = torch.empty(rows, dtype=torch.float32, device=x.device)
+        res2 = None
+        res_out = None
+        if residual is not None:
+            _need(residual, "residual")
+            res2 = residual.reshape(-1, cols).contiguous()
+            res_out = torch.empty_like(x2)
+        w = weight.contiguous()
+        _lib.check(lib.pico_rmsnorm_fwd(_lib.ptr(x2), _lib.ptr(res2), _lib.ptr(w), _lib.ptr(y), _lib.ptr(res_out),
+                                        _lib.ptr(rstd), rows, cols, float(eps), _lib.stream_of(x)), "pico_rmsnorm_fwd")
+        x_eff = res_out if res_out is not None else x2
+        ctx.save_for_backward(x_eff, w, rstd)
+        ctx.shape = shape
+        ctx.has_residual = residual is not None
+        ctx.prenorm = prenorm
+        y = y.view(shape)
+        if prenorm:
+            return y, (res_out if res_out is not None else x2).view(shape)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy, *rest):
+        x_eff, w, rstd = ctx.saved_tensors
+        cols = ctx.shape[-1]
+        rows = x_eff.shape[0]
+        dy2 = dy.reshape(-1, cols).contiguous()
+        dres = None
+        if ctx.prenorm and rest and rest[0] is not None:
+            dres = rest[0].reshape(-1, cols).contiguous()
+        lib = _lib.load()
+        dx = torch.empty_like(x_eff)
+        dw = torch.empty_like(w)
+        ws = torch.empty(lib.pico_rmsnorm_bwd_workspace_bytes(rows, cols), dtype=torch.uint8, device=dy.device)
+        _lib.check(lib.pico_rmsnorm_bwd(_lib.ptr(dy2), _lib.ptr(dres), _lib.ptr(x_eff), _lib.ptr(w), _lib.ptr(rstd),
+                                        _lib.ptr(dx), _lib.ptr(dw), _lib.ptr(ws), rows, cols, _lib.stream_of(dy)),
+                   "pico_rmsnorm_bwd")
+        dx = dx.view(ctx.shape)
+        return dx, (dx if ctx.has_residual else None), dw, None, None
+
+
+def rms_norm(x, weight, eps=1e-5, residual=None, prenorm=False):
+    return _RMSNormFn.apply(x, residual, weight, eps, prenorm)
+
+
+def layer_norm_fn(x, weight, bias, residual=None, x1=None, weight1=None, bias1=None, eps=1e-6, dropout_p=0.0,
+                  rowscale=None, prenorm=False, residual_in_fp32=False, is_rms_norm=False,
+                  return_dropout_mask=False):
+    """flash-attn 2.5 `layer_norm_fn` restricted to what picotron calls: RMS norm, no bias/dropout
+    (ref picotron/model.py:53-64). Returns y, or (y, residual_out) when prenorm=True."""
+    if not is_rms_norm:
+        raise NotImplementedError("picotron_amd.layer_norm_fn: only is_rms_norm=True is implemented")
+    if bias is not None or x1 is not None or weight1 is not None or bias1 is not None or rowscale is not None:
+        raise NotImplementedError("picotron_amd.layer_norm_fn: bias/x1/weight1/bias1/rowscale unsupported")
+    if dropout_p != 0.0 or return_dropout_mask:
+        raise NotImplementedError("picotron_amd.layer_norm_fn: dropout unsupported")
+    if residual_in_fp32:
+        raise NotImplementedError("picotron_amd.layer_norm_fn: residual_in_fp32 unsupported")
+    return _RMSNormFn.apply(x, residual, weight, eps, prenorm)
+
+
+# --------------------------------------------------------------------------------------------
+# Rotary embedding (flash_attn.layers.rotary.apply_rotary_emb, interleaved=False)
+# --------------------------------------------------------------------------------------------
+def _rope_launch(x, out, cos, sin, conjugate):
+    B, S, H, D = x.shape
+    lib = _lib.load()
+    _lib.check(lib.pico_rope(_lib.ptr(x), _lib.ptr(out), _lib.ptr(cos), _lib.ptr(sin), B, S, H, D,
+                             _lib.i64x3(x.stride()[:3]), _lib.i64x3(out.stride()[:3]), cos.stride(0),
+                             1 if conjugate else 0, _lib.stream_of(x)), "pico_rope")
+
+
+class _RotaryFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, cos, sin):
+        out = torch.empty(x.shape, dtype=x.dtype, device=x.device)
+        _rope_launch(x, out, cos, sin, False)
+        ctx.save_for_backward(cos, sin)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        cos, sin = ctx.saved_tensors
+        if dout.stride(-1) != 1:
+            dout = dout.contiguous()
+        dx = torch.empty(dout.shape, dtype=dout.dtype, device=dout.device)
+        _rope_launch(dout, dx, cos, sin, True)
+        return dx, None, None
+
+
+def apply_rotary_emb(x, cos, sin, interleaved=False, inplace=False, seqlen_offsets=0, cu_seqlens=None,
+                     max_seqlen=None):
+    """flash-attn `apply_rotary_emb`: x [B, S, H, D], cos/sin [S, D/2] (row stride free) -> [B, S, H, D]
+    (ref picotron/model.py:135-136)."""
+    if interleaved:
+        raise NotImplementedError("picotron_amd.apply_rotary_emb: interleaved=True unsupported")
+    if cu_seqlens is not None or max_seqlen is not None or (not isinstance(seqlen_offsets, int)) or seqlen_offsets:
+        raise NotImplementedError("picotron_amd.apply_rotary_emb: varlen / seqlen_offsets unsupported")
+    _need(x, "x")
+    _need(cos, "cos")
+    _need(sin, "sin")
+    if x.dim() != 4:
+        raise ValueError("apply_rotary_emb: x must be [batch, seqlen, heads, head_dim]")
+    B, S, H, D = x.shape
+    if cos.shape[0] < S or cos.shape[1] * 2 != D or sin.shape != cos.shape:
+        raise ValueError(f"apply_rotary_emb: cos/sin must be [>= {S}, {D // 2}], got {tuple(cos.shape)}")
+    if cos.stride(1) != 1 or sin.stride(1) != 1 or cos.stride(0) != sin.stride(0):
+        raise ValueError("apply_rotary_emb: cos/sin rows must be unit-stride with equal row strides")
+    if x.stride(-1) != 1:
+        x = x.contiguous()
+    out = _RotaryFn.apply(x, cos, sin)
+    if inplace:
+        with torch.no_grad():
+            x.copy_(out)
+        return x
+    return out
+
+
+# --------------------------------------------------------------------------------------------
+# SwiGLU epilogue
+# --------------------------------------------------------------------------------------------
+class _SwiGLUFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, gate, up):
+        _need(gate, "gate")
+        _need(up, "up")
+        if gate.shape != up.shape:
+            raise ValueError("swiglu: gate and up must have the same shape")
+        g = gate.contiguous()
+        u = up.contiguous()
+        out = torch.empty_like(g)
+        lib = _lib.load()
+        _lib.check(lib.pico_swiglu_fwd(_lib.ptr(g), _lib.ptr(u), _lib.ptr(out), g.numel(), _lib.stream_of(g)),
+                   "pico_swiglu_fwd")
+        ctx.save_for_backward(g, u)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        g, u = ctx.saved_tensors
+        d = dout.contiguous()
+        dg = torch.empty_like(g)
+        du = torch.empty_like(u)
+        lib = _lib.load()
+        _lib.check(lib.pico_swiglu_bwd(_lib.ptr(d), _lib.ptr(g), _lib.ptr(u), _lib.ptr(dg), _lib.ptr(du), g.numel(),
+                                       _lib.stream_of(d)), "pico_swiglu_bwd")
+        return dg, du
+
+
+def swiglu(gate, up):
+    """silu(gate) * up with one fused kernel each way (ref picotron/model.py:185)."""
+    return _SwiGLUFn.apply(gate, up)
+
+
+# --------------------------------------------------------------------------------------------
+# Flash attention
+# --------------------------------------------------------------------------------------------
+def _attn_args(q, k, v, o, lse, scale, causal):
+    a = _lib.AttnArgs()
+    a.q, a.k, a.v = _lib.ptr(q), _lib.ptr(k), _lib.ptr(v)
+    a.o, a.lse = _lib.ptr(o), _lib.ptr(lse)
+    B, Sq, Hq, D = q.shape
+    a.batch, a.seqlen_q, a.heads_q, a.head_dim = B, Sq, Hq, D
+    a.seqlen_k, a.heads_kv = k.shape[1], k.shape[2]
+    a.q_strides = _lib.i64x3(q.stride()[:3])
+    a.k_strides = _lib.i64x3(k.stride()[:3])
+    a.v_strides = _lib.i64x3(v.stride()[:3])
+    a.o_strides = _lib.i64x3(o.stride()[:3])
+    a.softmax_scale = float(scale)
+    a.causal = 1 if causal else 0
+    a.flags = 0
+    return a
+
+
+def _check_qkv(q, k, v):
+    for t, n in ((q, "q"), (k, "k"), (v, "v")):
+        _need(t, n)
+        if t.dim() != 4:
+            raise ValueError(f"flash attention: {n} must be [batch, seqlen, heads, head_dim]")
+        if t.stride(-1) != 1:
+            raise ValueError(f"flash attention: {n} must have unit last-dim stride")
+    if k.shape != v.shape or q.shape[0] != k.shape[0] or q.shape[3] != k.shape[3]:
+        raise ValueError("flash attention: incompatible q/k/v shapes")
+    if q.shape[3] not in (64, 128):
+        raise NotImplementedError(f"flash attention: head_dim {q.shape[3]} unsupported (64, 128)")
+    if q.shape[2] % k.shape[2] != 0:
+        raise ValueError("flash attention: heads_q must be a multiple of heads_kv")
+
+
+def attention_block_fwd(q, k, v, softmax_scale, causal):
+    """O [B,Sq,Hq,D] bf16 and LSE [B,Hq,Sq] fp32 (natural log) of softmax(scale*QK^T [+causal]) V."""
+    _check_qkv(q, k, v)
+    q, k, v = [t if t.stride(-1) == 1 and all(s % 8 == 0 for s in t.stride()[:3]) else t.contiguous()
+               for t in (q, k, v)]
+    B, Sq, Hq, D = q.shape
+    o = torch.empty((B, Sq, Hq, D), dtype=q.dtype, device=q.device)
+    lse = torch.empty((B, Hq, Sq), dtype=torch.float32, device=q.device)
+    a = _attn_args(q, k, v, o, lse, softmax_scale, causal)
+    _lib.check(_lib.load().pico_attn_fwd(ctypes.byref(a), _lib.stream_of(q)), "pico_attn_fwd")
+    return o, lse
+
+
+def attention_block_bwd(dout, q, k, v, o, lse, softmax_scale, causal, dq_accum=None):
+    """(dq, dk, dv) of attention given the (possibly global) O and LSE. If dq_accum (fp32
+    [B,Sq,Hq,D]) is given, dq is ADDED into it and returned instead of a bf16 dq."""
+    _check_qkv(q, k, v)
+    _need(dout, "dout")
+    if dout.stride(-1) != 1 or any(s % 8 for s in dout.stride()[:3]):
+        dout = dout.contiguous()
+    B, Sq, Hq, D = q.shape
+    dk = torch.empty(k.shape, dtype=k.dtype, device=k.device)
+    dv = torch.empty(v.shape, dtype=v.dtype, device=v.device)
+    a = _attn_args(q, k, v, o, lse, softmax_scale, causal)
+    a.dout = _lib.ptr(dout)
+    a.do_strides = _lib.i64x3(dout.stride()[:3])
+    if dq_accum is not None:
+        _need(dq_accum, "dq_accum", torch.float32)
+        dq = dq_accum
+        a.flags = _lib.ATTN_DQ_F32_ACCUM
+    else:
+        dq = torch.empty((B, Sq, Hq, D), dtype=q.dtype, device=q.device)
+    a.dq, a.dk, a.dv = _lib.ptr(dq), _lib.ptr(dk), _lib.ptr(dv)
+    a.dq_strides = _lib.i64x3(dq.stride()[:3])
+    a.dk_strides = _lib.i64x3(dk.stride()[:3])
+    a.dv_strides = _lib.i64x3(dv.stride()[:3])
+    lib = _lib.load()
+    ws = torch.empty(lib.pico_attn_bwd_workspace_bytes(ctypes.byref(a)), dtype=torch.uint8, device=q.device)
+    a.workspace = _lib.ptr(ws)
+    _lib.check(lib.pico_attn_bwd(ctypes.byref(a), _lib.stream_of(q)), "pico_attn_bwd")
+    return dq, dk, dv
+
+
+class _FlashAttnFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, k, v, softmax_scale, causal):
+        o, lse = attention_block_fwd(q, k, v, softmax_scale, causal)
+        ctx.save_for_backward(q, k, v, o, lse)
+        ctx.softmax_scale = softmax_scale
+        ctx.causal = causal
+        return o
+
+    @staticmethod
+    def backward(ctx, dout):
+        q, k, v, o, lse = ctx.saved_tensors
+        dq, dk, dv = attention_block_bwd(dout, q, k, v, o, lse, ctx.softmax_scale, ctx.causal)
+        return dq, dk, dv, None, None
+
+
+def flash_attn_func(q, k, v, dropout_p=0.0, softmax_scale=None, causal=False, window_size=(-1, -1),
+                    alibi_slopes=None, deterministic=False, return_attn_probs=False):
+    """flash-attn `flash_attn_func`: q [B,Sq,Hq,D], k/v [B,Sk,Hkv,D] -> out [B,Sq,Hq,D]
+    (ref picotron/model.py:32-36)."""
+    if dropout_p != 0.0:
+        raise NotImplementedError("picotron_amd.flash_attn_func: dropout unsupported")
+    if tuple(window_size) != (-1, -1) or alibi_slopes is not None or return_attn_probs:
+        raise NotImplementedError("picotron_amd.flash_attn_func: window/alibi/return_attn_probs unsupported")
+    if softmax_scale is None:
+        softmax_scale = 1.0 / math.sqrt(q.shape[-1])
+    return _FlashAttnFn.apply(q, k, v, float(softmax_scale), bool(causal))

@@ -1,0 +1,309 @@
+"""Parity of the gfx950 kernels (through the C ABI) with the CPU oracle and the reference goldens.
+
+Tolerances (bf16 outputs vs an fp64/fp32 oracle on the SAME bf16 inputs):
+  * elementwise/norm kernels (one bf16 rounding): rel-L2 <= 4e-3 and max-abs within 2 bf16 ulps of
+    the output magnitude, and never worse than the reference's own bf16 eager path (+1 ulp);
+  * attention fwd: rel-L2 <= 4e-3; bwd (dq/dk/dv): rel-L2 <= 1e-2 (P and dS are bf16 MFMA operands,
+    as in flash-attn) — the reference's bf16 eager SDPA error at these shapes is 3.4e-3 fwd;
+  * LSE (fp32): max-abs <= 2e-3;
+  * DP bucket kernels: bit-exact.
+"""
+import math
+
+import pytest
+import torch
+
+from conftest import max_abs, rel_l2
+from oracle import hotpath as H
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+BF = torch.bfloat16
+
+
+def _ops():
+    from picotron_amd import ops
+    return ops
+
+
+def _ulp_bound(ref, k=2.0):
+    # k bf16 ulps of the largest magnitude (2^-8 relative spacing)
+    return k * float(ref.abs().max()) * 2.0 ** -8
+
+
+# ------------------------------------------------------------------------------------------ RMSNorm
+def test_rmsnorm_golden(golden_kernels):
+    ops = _ops()
+    g = golden_kernels
+    x = g["rms.x"].to(DEV).requires_grad_(True)
+    w = g["rms.w"].to(DEV).requires_grad_(True)
+    y = ops.rms_norm(x, w, 1e-5)
+    yref = g["rms.y_f64"]
+    assert rel_l2(y.cpu(), yref) < 4e-3
+    eager_err = max_abs(g["rms.y_eager_bf16"], yref)
+    assert max_abs(y.detach().cpu(), yref) <= eager_err + _ulp_bound(yref, 1)
+    y.backward(g["rms.dy"].to(DEV).to(BF))
+    dx, dw = H.rmsnorm_grads(g["rms.x"], g["rms.w"], 1e-5, g["rms.dy"].to(BF).double())
+    assert rel_l2(x.grad.cpu(), dx) < 4e-3
+    assert rel_l2(w.grad.cpu(), dw) < 4e-3
+
+
+@pytest.mark.parametrize("rows,cols", [(1, 64), (7, 128), (4096, 2048), (333, 4096), (5, 8192), (64, 1000 * 8)])
+def test_rmsnorm_shapes(rows, cols):
+    ops = _ops()
+    torch.manual_seed(rows + cols)
+    x = torch.randn(rows, cols, dtype=BF, device=DEV) * 3
+    w = (1 + 0.1 * torch.randn(cols, device=DEV)).to(BF)
+    y = ops.rms_norm(x, w, 1e-5)
+    yref, _ = H.rmsnorm_fused(x.cpu().double(), w.cpu().double(), 1e-5)
+    assert rel_l2(y.cpu(), yref) < 4e-3
+    assert max_abs(y.cpu(), yref) <= _ulp_bound(yref, 2)
+    if cols <= 4096:
+        xr = x.clone().requires_grad_(True)
+        wr = w.clone().requires_grad_(True)
+        dy = torch.randn(rows, cols, dtype=BF, device=DEV)
+        ops.rms_norm(xr, wr, 1e-5).backward(dy)
+        dx, dw = H.rmsnorm_grads(x.cpu(), w.cpu(), 1e-5, dy.cpu().double())
+        assert rel_l2(xr.grad.cpu(), dx) < 4e-3
+        assert rel_l2(wr.grad.cpu(), dw) < 4e-3
+
+
+def test_rmsnorm_residual_prenorm():
+    ops = _ops()
+    torch.manual_seed(1)
+    x = torch.randn(64, 2048, dtype=BF, device=DEV, requires_grad=True)
+    r = torch.randn(64, 2048, dtype=BF, device=DEV, requires_grad=True)
+    w = (1 + 0.1 * torch.randn(2048, device=DEV)).to(BF).requires_grad_(True)
+    y, res = ops.layer_norm_fn(x, w, None, residual=r, eps=1e-5, prenorm=True, is_rms_norm=True)
+    yref, xe = H.rmsnorm_fused(x.detach().cpu(), w.detach().cpu(), 1e-5, residual=r.detach().cpu())
+    assert torch.equal(res.cpu(), xe)  # residual_out = bf16(x + r), bit-exact
+    assert max_abs(y.detach().cpu(), yref.double()) <= _ulp_bound(yref.double(), 1)
+    dy = torch.randn_like(y)
+    dres = torch.randn_like(res)
+    torch.autograd.backward([y, res], [dy, dres])
+    dxe, dw = H.rmsnorm_grads(xe, w.detach().cpu(), 1e-5, dy.cpu().double())
+    assert rel_l2(x.grad.cpu(), dxe + dres.cpu().double()) < 4e-3
+    assert torch.equal(x.grad, r.grad)
+
+
+def test_rmsnorm_rejects_cpu_tensors():
+    ops = _ops()
+    with pytest.raises(RuntimeError):
+        ops.rms_norm(torch.randn(4, 64, dtype=BF), torch.ones(64, dtype=BF))
+
+
+# ------------------------------------------------------------------------------------------ RoPE
+def test_rope_golden(golden_kernels):
+    ops = _ops()
+    g = golden_kernels
+    cos, sin = g["rope.cos"].to(DEV), g["rope.sin"].to(DEV)
+    q = g["rope.q"].transpose(1, 2).contiguous().to(DEV).requires_grad_(True)  # [B,S,H,D]
+    out = ops.apply_rotary_emb(q, cos[:, :32], sin[:, :32])
+    ref = g["rope.out_f64"].transpose(1, 2)
+    assert rel_l2(out.detach().cpu(), ref) < 4e-3
+    assert max_abs(out.detach().cpu(), ref) <= max_abs(g["rope.out_eager_bf16"], g["rope.out_f64"]) + _ulp_bound(ref, 1)
+    out.backward(g["rope.dy"].transpose(1, 2).to(DEV).to(BF))
+    assert rel_l2(q.grad.cpu(), g["rope.dx_f64"].transpose(1, 2)) < 4e-3
+
+
+@pytest.mark.parametrize("B,S,H,D", [(4, 1024, 32, 64), (1, 100, 3, 128), (2, 37, 8, 64)])
+def test_rope_shapes_and_strides(B, S, H, D):
+    ops = _ops()
+    torch.manual_seed(S)
+    cos, sin = H.get_cos_sin(S, D, base=10000.0)
+    big = torch.randn(B, S, H + 2, D, dtype=BF, device=DEV)
+    x = big[:, :, 1:H + 1]  # non-contiguous head slice (row stride (H+2)*D)
+    out = ops.apply_rotary_emb(x, cos.to(DEV)[:, : D // 2], sin.to(DEV)[:, : D // 2])
+    ref = H.rope_fused(x.cpu().double(), cos.double(), sin.double())
+    assert rel_l2(out.cpu(), ref) < 4e-3
+    assert max_abs(out.cpu(), ref) <= _ulp_bound(ref, 2)
+    # in-place aliasing (out == x)
+    y = x.clone()
+    ops.apply_rotary_emb(y, cos.to(DEV)[:, : D // 2], sin.to(DEV)[:, : D // 2], inplace=True)
+    assert torch.equal(y, out)
+
+
+# ------------------------------------------------------------------------------------------ SwiGLU
+def test_swiglu_golden(golden_kernels):
+    ops = _ops()
+    g = golden_kernels
+    gg = g["swiglu.g"].to(DEV).requires_grad_(True)
+    uu = g["swiglu.u"].to(DEV).requires_grad_(True)
+    h = ops.swiglu(gg, uu)
+    ref = g["swiglu.h_f64"]
+    assert rel_l2(h.detach().cpu(), ref) < 4e-3
+    assert max_abs(h.detach().cpu(), ref) <= max_abs(g["swiglu.h_eager_bf16"], ref) + _ulp_bound(ref, 1)
+    h.backward(g["swiglu.dh"].to(DEV).to(BF))
+    dg, du = H.swiglu_grads(g["swiglu.g"], g["swiglu.u"], g["swiglu.dh"].to(BF))
+    assert rel_l2(gg.grad.cpu(), dg) < 4e-3 and rel_l2(uu.grad.cpu(), du) < 4e-3
+
+
+@pytest.mark.parametrize("n", [1, 7, 8, 4096 * 8192 // 16, 12345])
+def test_swiglu_sizes(n):
+    ops = _ops()
+    torch.manual_seed(n)
+    g = torch.randn(n, dtype=BF, device=DEV) * 2
+    u = torch.randn(n, dtype=BF, device=DEV)
+    h = ops.swiglu(g, u)
+    ref = H.swiglu(g.cpu().double(), u.cpu().double())
+    assert rel_l2(h.cpu(), ref) < 4e-3
+
+
+# ------------------------------------------------------------------------------------------ attention
+@pytest.mark.parametrize("tag", ["causal", "full"])
+def test_attention_golden(golden_kernels, tag):
+    ops = _ops()
+    g = golden_kernels
+    p = lambda n: g[f"attn.{tag}.{n}"]
+    to = lambda t: t.to(BF).transpose(1, 2).contiguous().to(DEV)  # [B,H,S,D] fp32 -> [B,S,H,D] bf16
+    q, k, v = to(p("q")), to(p("k")), to(p("v"))
+    sc = 1.0 / math.sqrt(64)
+    o, lse = ops.attention_block_fwd(q, k, v, sc, tag == "causal")
+    # oracle on the same bf16-rounded inputs
+    qb, kb, vb = [p(n).to(BF).double() for n in ("q", "k", "v")]
+    O, L = H.attention_fwd(qb, kb, vb, sc, tag == "causal")
+    assert rel_l2(o.transpose(1, 2).cpu(), O) < 4e-3
+    assert max_abs(lse.cpu(), L) < 2e-3
+    assert rel_l2(o.transpose(1, 2).cpu(), p("o")) < 1e-2  # vs the reference's fp32 output
+    do = to(p("do"))
+    dq, dk, dv = ops.attention_block_bwd(do, q, k, v, o, lse, sc, tag == "causal")
+    dQ, dK, dV = H.attention_bwd(p("do").to(BF).double(), qb, kb, vb, o.transpose(1, 2).cpu().double(),
+                                 lse.cpu().double(), sc, tag == "causal")
+    for a, b in ((dq, dQ), (dk, dK), (dv, dV)):
+        assert rel_l2(a.transpose(1, 2).cpu(), b) < 1e-2
+
+
+CASES = [
+    # B, Sq, Sk, Hq, Hkv, D, causal
+    (1, 128, 128, 2, 2, 64, True),
+    (2, 1024, 1024, 4, 4, 64, True),   # C2 geometry slice
+    (1, 257, 257, 4, 2, 64, True),     # ragged + GQA 2
+    (1, 1000, 1000, 8, 2, 128, True),  # D=128, GQA 4, ragged
+    (2, 96, 200, 4, 4, 64, False),     # cross lengths, non-causal
+    (1, 300, 77, 2, 1, 128, False),
+    (1, 1, 1, 1, 1, 64, True),
+]
+
+
+@pytest.mark.parametrize("B,Sq,Sk,Hq,Hkv,D,causal", CASES)
+def test_attention_vs_oracle(B, Sq, Sk, Hq, Hkv, D, causal):
+    ops = _ops()
+    torch.manual_seed(Sq * 7 + Sk + D)
+    q = torch.randn(B, Sq, Hq, D, dtype=BF, device=DEV)
+    k = torch.randn(B, Sk, Hkv, D, dtype=BF, device=DEV)
+    v = torch.randn(B, Sk, Hkv, D, dtype=BF, device=DEV)
+    do = torch.randn(B, Sq, Hq, D, dtype=BF, device=DEV)
+    sc = 1.0 / math.sqrt(D)
+    o, lse = ops.attention_block_fwd(q, k, v, sc, causal)
+    qd, kd, vd = [t.transpose(1, 2).cpu().double() for t in (q, k, v)]
+    O, L = H.attention_fwd(qd, kd, vd, sc, causal)
+    assert rel_l2(o.transpose(1, 2).cpu(), O) < 4e-3
+    assert max_abs(lse.cpu(), L) < 2e-3
+    dq, dk, dv = ops.attention_block_bwd(do, q, k, v, o, lse, sc, causal)
+    dQ, dK, dV = H.attention_bwd(do.transpose(1, 2).cpu().double(), qd, kd, vd, o.transpose(1, 2).cpu().double(),
+                                 lse.cpu().double(), sc, causal)
+    assert rel_l2(dq.transpose(1, 2).cpu(), dQ) < 1e-2
+    assert rel_l2(dk.transpose(1, 2).cpu(), dK) < 1e-2
+    assert rel_l2(dv.transpose(1, 2).cpu(), dV) < 1e-2
+
+
+def test_attention_dq_f32_accumulate():
+    ops = _ops()
+    torch.manual_seed(3)
+    q, k, v, do = [torch.randn(1, 256, 2, 64, dtype=BF, device=DEV) for _ in range(4)]
+    o, lse = ops.attention_block_fwd(q, k, v, 0.125, True)
+    dq_bf, _, _ = ops.attention_block_bwd(do, q, k, v, o, lse, 0.125, True)
+    acc = torch.full(q.shape, 0.5, dtype=torch.float32, device=DEV)
+    ops.attention_block_bwd(do, q, k, v, o, lse, 0.125, True, dq_accum=acc)
+    assert rel_l2((acc - 0.5).cpu(), dq_bf.float().cpu()) < 4e-3
+
+
+def test_attention_strided_bhsd_views():
+    """The reference hands flash-attn k/v as [B,S,H,D] views of BHSD tensors (ref model.py:33-35)."""
+    ops = _ops()
+    torch.manual_seed(5)
+    q = torch.randn(2, 4, 128, 64, dtype=BF, device=DEV)
+    k = torch.randn(2, 4, 128, 64, dtype=BF, device=DEV)
+    v = torch.randn(2, 4, 128, 64, dtype=BF, device=DEV)
+    o1 = ops.flash_attn_func(q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2), causal=True)
+    o2 = ops.flash_attn_func(q.transpose(1, 2).contiguous(), k.transpose(1, 2).contiguous(),
+                             v.transpose(1, 2).contiguous(), causal=True)
+    assert torch.equal(o1, o2)
+
+
+def test_attention_softmax_rescale_branch():
+    """A spiked key forces the running max to jump mid-sweep (rule 26)."""
+    ops = _ops()
+    torch.manual_seed(9)
+    q = torch.randn(1, 512, 2, 64, dtype=BF, device=DEV)
+    k = torch.randn(1, 512, 2, 64, dtype=BF, device=DEV)
+    v = torch.randn(1, 512, 2, 64, dtype=BF, device=DEV)
+    k[:, 300] = q[:, 400] * 4  # row 400 sees a huge score at key 300 (tile 4 of 8)
+    o, lse = ops.attention_block_fwd(q, k, v, 0.125, True)
+    O, L = H.attention_fwd(*[t.transpose(1, 2).cpu().double() for t in (q, k, v)], 0.125, True)
+    assert rel_l2(o.transpose(1, 2).cpu(), O) < 4e-3
+    assert max_abs(o.transpose(1, 2).cpu(), O) < 2e-2
+
+
+# ------------------------------------------------------------------------------------------ ring merge
+def test_merge_golden(golden_kernels):
+    from picotron_amd.context_parallel.context_parallel import update_out_and_lse
+    g = golden_kernels
+    out = lse = None
+    for i in range(3):
+        bo = g[f"merge.block_out{i}"].transpose(1, 2).contiguous().to(BF).to(DEV)  # [B,S,H,D]
+        out, lse = update_out_and_lse(out, lse, bo, g[f"merge.block_lse{i}"].to(DEV))
+    ref_out, ref_lse = None, None
+    for i in range(3):
+        ref_out, ref_lse = H.update_out_and_lse(ref_out, ref_lse, g[f"merge.block_out{i}"].to(BF).double(),
+                                                g[f"merge.block_lse{i}"].double())
+    assert max_abs(out.transpose(1, 2).cpu(), ref_out) < 1e-5
+    assert max_abs(lse.cpu(), ref_lse.squeeze(-1)) < 1e-5
+
+
+def test_ring_attention_single_process_blocks():
+    """Causal attention over a sequence split in 4 blocks, merged with the kernels the way the ring
+    does (step s computes q_r against kv_{r-s}), equals whole-sequence attention."""
+    ops = _ops()
+    from picotron_amd.context_parallel.context_parallel import update_out_and_lse
+    torch.manual_seed(11)
+    B, S, Hh, D, W = 1, 512, 2, 64, 4
+    q, k, v = [torch.randn(B, S, Hh, D, dtype=BF, device=DEV) for _ in range(3)]
+    full, _ = ops.attention_block_fwd(q, k, v, 0.125, True)
+    n = S // W
+    for r in range(W):
+        out = lse = None
+        for step in range(r + 1):
+            src = r - step
+            bo, bl = ops.attention_block_fwd(q[:, r * n:(r + 1) * n], k[:, src * n:(src + 1) * n],
+                                             v[:, src * n:(src + 1) * n], 0.125, step == 0)
+            out, lse = update_out_and_lse(out, lse, bo, bl)
+        assert rel_l2(out.cpu(), full[:, r * n:(r + 1) * n].float().cpu()) < 4e-3
+
+
+# ------------------------------------------------------------------------------------------ DP kernels
+def test_grad_accum_and_cast_bit_exact():
+    from picotron_amd.data_parallel.bucket import HipBucketKernels as K
+    torch.manual_seed(0)
+    for n in (1, 7, 8, 1000003, 4096 * 2048):
+        m = torch.randn(n, device=DEV)
+        g = torch.randn(n, device=DEV).to(BF)
+        ref = m.clone().add_(g)
+        K.accumulate(m, g, 1)
+        assert torch.equal(m, ref)
+        ref = (m.clone().add_(g)) / 8
+        K.accumulate(m, g, 8)
+        assert torch.equal(m, ref)
+        ref = m.clone() / 3
+        K.scale(m, 3)
+        assert torch.equal(m, ref)
+        out = torch.empty(n, dtype=BF, device=DEV)
+        K.cast(m, out)
+        assert torch.equal(out, m.to(BF))
+    # unaligned views (param offsets inside a bucket)
+    big = torch.randn(1000, device=DEV)
+    gg = torch.randn(1000, device=DEV).to(BF)
+    v = big[3:803]
+    ref = v.clone().add_(gg[3:803])
+    K.accumulate(v, gg[3:803], 1)
+    assert torch.equal(v, ref)
