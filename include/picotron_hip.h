@@ -137,9 +137,10 @@ int pico_attn_merge(float* out, float* lse, const void* block_out, const float* 
                     void* stream);
 
 /* ---- DP gradient buckets ---- */
-/* main_grad[i] = (main_grad[i] + float(grad[i])) / divide_by   (divide_by == 1: no division) */
+/* main_grad[i] = (main_grad[i] + float(grad[i])) * (1.0f / divide_by)   (divide_by == 1: no scaling).
+ * The fp32 reciprocal product is what ATen computes for the reference's `grad_data /= W` on a GPU. */
 int pico_grad_accum(float* main_grad, const void* grad, int64_t n, float divide_by, void* stream);
-/* buf[i] = buf[i] / divide_by */
+/* buf[i] = buf[i] * (1.0f / divide_by) */
 int pico_scale_f32(float* buf, int64_t n, float divide_by, void* stream);
 /* dst[i] = bf16(src[i]) (round to nearest even) */
 int pico_cast_f32_bf16(const float* src, void* dst, int64_t n, void* stream);

@@ -202,7 +202,8 @@ def bucket_size_elems(bucket_cap_mb=25, grad_type=torch.float32):
 
 class CpuBucketKernels:
     """CPU device-op table for picotron_amd.data_parallel.bucket in gloo tests: exactly the
-    reference's ATen ops (add_ then /=, ref data_parallel.py:131 / bucket.py:30; .to(dtype) :165)."""
+    reference's ATen ops (add_ then /=, ref data_parallel.py:131 / bucket.py:30; .to(dtype) :165).
+    (On CPU ATen divides; on a GPU it multiplies by fp32(1/W) — equal for power-of-two W.)"""
 
     @staticmethod
     def accumulate(main_grad, grad, divide_by):

@@ -9,7 +9,8 @@ import os
 
 import torch
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libpicotron_hip.so")
+LIB_PATH = os.environ.get("PICO_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib",
+                                                           "libpicotron_hip.so")
 
 # kernel ids (enum in include/picotron_hip.h)
 K_RMSNORM_FWD, K_RMSNORM_BWD, K_RMSNORM_DW, K_ROPE = 1, 2, 3, 4

@@ -38,7 +38,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const pico_attn_args a
   __shared__ __attribute__((aligned(16))) FwdSmem<D> sm;
 
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (scalar branches)
   const int r = lane & 31, h = lane >> 5;
 
   // LPT order: heaviest query blocks of every head first.
@@ -65,12 +65,11 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const pico_attn_args a
   bf16x8 qf[KS];
   {
     const bool ok = my_q < Sq;
-    const bf16_t* qp = qg + (int64_t)(ok ? my_q : 0) * a.q_strides[1] + 8 * h;
+    const bf16_t* qp = qg + (int64_t)min(my_q, Sq - 1) * a.q_strides[1] + 8 * h;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
-      u16x8 v = *reinterpret_cast<const u16x8*>(qp + 16 * ks);
-      if (!ok) v = (u16x8)0;
-      qf[ks] = __builtin_bit_cast(bf16x8, v);
+      const u16x8 v = *reinterpret_cast<const u16x8*>(qp + 16 * ks);
+      qf[ks] = __builtin_bit_cast(bf16x8, ok ? v : (u16x8)0);
     }
   }
 
@@ -80,30 +79,28 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const pico_attn_args a
   const int ntiles = (kend + BN - 1) / BN;
 
   // ---- register staging of K/V tiles ----
+  // Loads are issued unconditionally from a clamped row; the zero-fill of rows past Sk is applied
+  // when the registers are written to LDS, so no wait is forced right after the loads.
   u16x8 kreg[CHUNKS_PER_THREAD], vreg[CHUNKS_PER_THREAD];
   auto gload = [&](int tile) {
 #pragma unroll
     for (int c = 0; c < CHUNKS_PER_THREAD; ++c) {
       const int id = threadIdx.x + 256 * c;
       const int row = id / CPR, ch = id % CPR;
-      const int key = tile * BN + row;
-      if (key < Sk) {
-        kreg[c] = *reinterpret_cast<const u16x8*>(kg + (int64_t)key * ksd + ch * 8);
-        vreg[c] = *reinterpret_cast<const u16x8*>(vg + (int64_t)key * vsd + ch * 8);
-      } else {
-        kreg[c] = (u16x8)0;
-        vreg[c] = (u16x8)0;
-      }
+      const int kc = min(tile * BN + row, Sk - 1);
+      kreg[c] = *reinterpret_cast<const u16x8*>(kg + (int64_t)kc * ksd + ch * 8);
+      vreg[c] = *reinterpret_cast<const u16x8*>(vg + (int64_t)kc * vsd + ch * 8);
     }
   };
-  auto swrite = [&](int buf) {
+  auto swrite = [&](int buf, int tile) {
 #pragma unroll
     for (int c = 0; c < CHUNKS_PER_THREAD; ++c) {
       const int id = threadIdx.x + 256 * c;
       const int row = id / CPR, ch = id % CPR;
+      const bool ok = tile * BN + row < Sk;
       const int off = lds_off<D>(row, ch);
-      *reinterpret_cast<u16x8*>(sm.k[buf] + off) = kreg[c];
-      *reinterpret_cast<u16x8*>(sm.v[buf] + off) = vreg[c];
+      *reinterpret_cast<u16x8*>(sm.k[buf] + off) = ok ? kreg[c] : (u16x8)0;
+      *reinterpret_cast<u16x8*>(sm.v[buf] + off) = ok ? vreg[c] : (u16x8)0;
     }
   };
 
@@ -114,7 +111,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const pico_attn_args a
 
   if (ntiles > 0) {
     gload(0);
-    swrite(0);
+    swrite(0, 0);
   }
   __syncthreads();
 
@@ -148,7 +145,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const pico_attn_args a
           float x = s[kt][i] * scale_log2;
           if (need_mask) {
             const int key = n0 + kt * 32 + acc_row(i, h);
-            if (key >= Sk || (CAUSAL && key > my_q)) x = -INFINITY;
+            x = (key >= Sk || (CAUSAL && key > my_q)) ? -INFINITY : x;
           }
           s[kt][i] = x;
           mloc = fmaxf(mloc, x);
@@ -189,7 +186,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const pico_attn_args a
         }
       }
     }
-    if (more) swrite(buf ^ 1);
+    if (more) swrite(buf ^ 1, t + 1);
     __syncthreads();
   }
 

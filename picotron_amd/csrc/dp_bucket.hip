@@ -2,9 +2,10 @@
 //
 // pico_grad_accum    : main_grad += grad (fp32 += bf16), ref picotron/data_parallel/data_parallel.py:131.
 //                      On the syncing micro-batch the bucket pre-scale grad_data /= W
-//                      (ref picotron/data_parallel/bucket.py:30) is folded in: (m + g) / W is the same
-//                      two correctly-rounded fp32 ops as the reference's add_ followed by /=, so the
-//                      result is bit-identical while the bucket is read and written once instead of twice.
+//                      (ref picotron/data_parallel/bucket.py:30) is folded in. On the GPU, ATen evaluates
+//                      `tensor /= python_scalar` as tensor * fp32(1/W) (its scalar-divisor fast path), so
+//                      (m + g) * fp32(1/W) is the same two correctly-rounded fp32 ops as the reference's
+//                      add_ followed by /=: bit-identical, with the bucket read and written once.
 // pico_scale_f32     : grad_data /= W for buckets whose params were accumulated unscaled.
 // pico_cast_f32_bf16 : p.grad = p.main_grad.to(bf16) (ref data_parallel.py:165), one launch per bucket.
 //
@@ -14,7 +15,7 @@
 namespace {
 
 __global__ __launch_bounds__(256) void grad_accum_vec(float* __restrict__ m, const bf16_t* __restrict__ g, int64_t nv,
-                                                      float div, int do_div) {
+                                                      float inv, int do_div) {
   const int64_t stride = (int64_t)gridDim.x * 256;
   for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < nv; t += stride) {
     const u16x8 gv = reinterpret_cast<const u16x8*>(g)[t];
@@ -25,8 +26,8 @@ __global__ __launch_bounds__(256) void grad_accum_vec(float* __restrict__ m, con
       a[j] = a[j] + bf2f(gv[j]);
       b[j] = b[j] + bf2f(gv[4 + j]);
       if (do_div) {
-        a[j] = a[j] / div;
-        b[j] = b[j] / div;
+        a[j] = a[j] * inv;
+        b[j] = b[j] * inv;
       }
     }
     reinterpret_cast<f32x4*>(m)[2 * t] = a;
@@ -35,27 +36,27 @@ __global__ __launch_bounds__(256) void grad_accum_vec(float* __restrict__ m, con
 }
 
 __global__ __launch_bounds__(256) void grad_accum_scalar(float* __restrict__ m, const bf16_t* __restrict__ g, int64_t n,
-                                                         float div, int do_div) {
+                                                         float inv, int do_div) {
   const int64_t stride = (int64_t)gridDim.x * 256;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
     float v = m[i] + bf2f(g[i]);
-    if (do_div) v = v / div;
+    if (do_div) v = v * inv;
     m[i] = v;
   }
 }
 
-__global__ __launch_bounds__(256) void scale_kernel(float* __restrict__ m, int64_t n, float div) {
+__global__ __launch_bounds__(256) void scale_kernel(float* __restrict__ m, int64_t n, float inv) {
   const int64_t stride = (int64_t)gridDim.x * 256;
   const int64_t nv = n / 4;
   for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < nv; t += stride) {
     f32x4 a = reinterpret_cast<const f32x4*>(m)[t];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) a[j] = a[j] / div;
+    for (int j = 0; j < 4; ++j) a[j] = a[j] * inv;
     reinterpret_cast<f32x4*>(m)[t] = a;
   }
   if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
     const int64_t i = nv * 4 + threadIdx.x;
-    m[i] = m[i] / div;
+    m[i] = m[i] * inv;
   }
 }
 
@@ -96,13 +97,14 @@ int pico_grad_accum(float* main_grad, const void* grad, int64_t n, float divide_
   if (n <= 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   const int do_div = divide_by != 1.f;
+  const float inv = 1.f / divide_by;  // fp32 reciprocal, as ATen's scalar-divisor path computes it
   const bool vec = n % 8 == 0 && (uintptr_t)main_grad % 32 == 0 && (uintptr_t)grad % 16 == 0;
   if (vec) {
     PICO_LAUNCH(PICO_K_GRAD_ACCUM, "grad_accum", s,
-                grad_accum_vec<<<grid_for(n / 8), 256, 0, s>>>(main_grad, (const bf16_t*)grad, n / 8, divide_by, do_div));
+                grad_accum_vec<<<grid_for(n / 8), 256, 0, s>>>(main_grad, (const bf16_t*)grad, n / 8, inv, do_div));
   } else {
     PICO_LAUNCH(PICO_K_GRAD_ACCUM, "grad_accum", s,
-                grad_accum_scalar<<<grid_for(n), 256, 0, s>>>(main_grad, (const bf16_t*)grad, n, divide_by, do_div));
+                grad_accum_scalar<<<grid_for(n), 256, 0, s>>>(main_grad, (const bf16_t*)grad, n, inv, do_div));
   }
   return 0;
 }
@@ -113,7 +115,7 @@ int pico_scale_f32(float* buf, int64_t n, float divide_by, void* stream) {
   PICO_REQUIRE((uintptr_t)buf % 16 == 0, "pico_scale_f32: buffer must be 16-byte aligned");
   if (n <= 0 || divide_by == 1.f) return 0;
   hipStream_t s = (hipStream_t)stream;
-  PICO_LAUNCH(PICO_K_SCALE, "scale_f32", s, scale_kernel<<<grid_for(n / 4), 256, 0, s>>>(buf, n, divide_by));
+  PICO_LAUNCH(PICO_K_SCALE, "scale_f32", s, scale_kernel<<<grid_for(n / 4), 256, 0, s>>>(buf, n, 1.f / divide_by));
   return 0;
 }
 

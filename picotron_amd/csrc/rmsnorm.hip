@@ -146,13 +146,27 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const bf16_t* __restri
   }
 }
 
+// dw[col] = sum over the workgroup partials, in a fixed order (deterministic): a 256-thread
+// workgroup covers 32 columns x 8 row-slices; each thread sums its slice (loads coalesced across the
+// 32 columns), then the 8 slices are combined through LDS in slice order.
 __global__ __launch_bounds__(256) void rmsnorm_dw_kernel(const float* __restrict__ part, bf16_t* __restrict__ dw, int nblk,
                                                          int cols) {
-  const int col = blockIdx.x * 256 + threadIdx.x;
-  if (col >= cols) return;
+  __shared__ float red[8][32];
+  const int c = threadIdx.x & 31, sl = threadIdx.x >> 5;
+  const int col = blockIdx.x * 32 + c;
   float s = 0.f;
-  for (int b = 0; b < nblk; ++b) s += part[(int64_t)b * cols + col];
-  dw[col] = f2bf(s);
+  if (col < cols) {
+#pragma unroll 8
+    for (int b = sl; b < nblk; b += 8) s += part[(int64_t)b * cols + col];
+  }
+  red[sl][c] = s;
+  __syncthreads();
+  if (sl == 0 && col < cols) {
+    float t = red[0][c];
+#pragma unroll
+    for (int k = 1; k < 8; ++k) t += red[k][c];
+    dw[col] = f2bf(t);
+  }
 }
 
 int maxc_for(int64_t cols) {
@@ -165,9 +179,9 @@ int maxc_for(int64_t cols) {
   return -1;
 }
 
-int bwd_blocks(int64_t rows) {
+int bwd_blocks(int64_t rows) {  // one workgroup per CU at most: fewer dw partial rows to reduce
   int64_t nb = (rows + WAVES - 1) / WAVES;
-  return (int)(nb < 512 ? nb : 512);
+  return (int)(nb < 256 ? nb : 256);
 }
 
 }  // namespace
@@ -228,7 +242,7 @@ int pico_rmsnorm_bwd(const void* dy, const void* dresidual, const void* x, const
   }
 #undef BWD_CASE
   PICO_LAUNCH(PICO_K_RMSNORM_DW, "rmsnorm_dw", s,
-              rmsnorm_dw_kernel<<<pico_cdiv(cols, 256), 256, 0, s>>>(part, (bf16_t*)dweight, nb, c));
+              rmsnorm_dw_kernel<<<pico_cdiv(cols, 32), 256, 0, s>>>(part, (bf16_t*)dweight, nb, c));
   return 0;
 }
 

@@ -1,0 +1,72 @@
+"""Attention kernel micro-benchmark at the SmolLM-1.7B shape (B=4, S=1024, H=32, D=64, causal) and
+optionally D=128 / GQA. Times every kernel id live with the library's HIP-event timer and prints
+one JSON line per config (TFLOP/s against the algorithmic causal FLOPs).
+
+  python scripts/attn_bench.py [--iters 50] [--configs c2,d128]
+  PICO_LIB_PATH=... selects an alternative build of the library (ablation variants).
+"""
+import argparse
+import json
+import math
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+CONFIGS = {
+    "c2": (4, 1024, 32, 32, 64, True),
+    "c2_full": (4, 1024, 32, 32, 64, False),
+    "d128": (2, 1024, 16, 16, 128, True),   # Llama-2-7B per TP rank (tp2), micro-batch 2
+    "gqa4": (4, 1024, 32, 8, 64, True),
+    "s4096": (1, 4096, 32, 32, 64, True),   # CP block size of config 5
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--configs", default="c2,d128")
+    args = ap.parse_args()
+    from picotron_amd import _lib as L
+    from picotron_amd import ops
+    L.load()
+    for name in args.configs.split(","):
+        B, S, Hq, Hkv, D, causal = CONFIGS[name]
+        torch.manual_seed(0)
+        q = torch.randn(B, S, Hq, D, dtype=torch.bfloat16, device="cuda")
+        k = torch.randn(B, S, Hkv, D, dtype=torch.bfloat16, device="cuda")
+        v = torch.randn(B, S, Hkv, D, dtype=torch.bfloat16, device="cuda")
+        do = torch.randn(B, S, Hq, D, dtype=torch.bfloat16, device="cuda")
+        sc = 1 / math.sqrt(D)
+        for _ in range(3):
+            o, lse = ops.attention_block_fwd(q, k, v, sc, causal)
+            ops.attention_block_bwd(do, q, k, v, o, lse, sc, causal)
+        torch.cuda.synchronize()
+        ids = [L.K_ATTN_FWD, L.K_ATTN_BWD_PRE, L.K_ATTN_BWD, L.K_ATTN_BWD_DQ]
+        for i in ids:
+            L.prof_enable(i, args.iters + 4)
+        for _ in range(args.iters):
+            o, lse = ops.attention_block_fwd(q, k, v, sc, causal)
+            ops.attention_block_bwd(do, q, k, v, o, lse, sc, causal)
+        torch.cuda.synchronize()
+        fl = 4.0 * B * Hq * S * S * D * (0.5 if causal else 1.0)
+        res = {"config": name, "B": B, "S": S, "Hq": Hq, "Hkv": Hkv, "D": D, "causal": causal}
+        tot_bwd = 0.0
+        for i in ids:
+            ms, n = L.prof_collect(i)
+            us = 1e3 * ms / max(n, 1)
+            res[L.KERNEL_NAMES[i] + "_us"] = round(us, 2)
+            if i != L.K_ATTN_FWD:
+                tot_bwd += us
+        L.load().pico_prof_enable(0, 0)
+        res["fwd_tflops"] = round(fl / (res["attn_fwd_us"] * 1e-6) / 1e12, 1)
+        res["bwd_kernel_tflops"] = round(2.5 * fl / (res["attn_bwd_us"] * 1e-6) / 1e12, 1)
+        res["bwd_total_tflops"] = round(2.5 * fl / (tot_bwd * 1e-6) / 1e12, 1)
+        res["fwd_bwd_tflops"] = round(3.5 * fl / ((res["attn_fwd_us"] + tot_bwd) * 1e-6) / 1e12, 1)
+        print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -262,33 +262,45 @@ def gen_loss_curve(M, steps=200):
     model = init_model_with_materialized_weights(model, cfg, save_dir=sft_dir)
     model.to(torch.float32)
     init = {k: v.detach().clone() for k, v in model.state_dict().items()}
-    opt = torch.optim.AdamW(model.parameters(), lr=1e-3)
     gen = torch.Generator().manual_seed(1234)
     mbs, seq, grad_acc = 4, 128, 2
     batches = [synth_tokens(mbs, seq + 1, V, gen, "arith") for _ in range(16)]
-    losses = []
-    k = 0
-    for step in range(steps):
-        opt.zero_grad()
-        acc = 0.0
-        for _ in range(grad_acc):
-            toks = batches[k % len(batches)]
-            k += 1
-            logits = model(input_ids=toks[:, :-1])
-            loss = torch.nn.functional.cross_entropy(logits.reshape(-1, V), toks[:, 1:].reshape(-1),
-                                                     reduction="mean") / grad_acc
-            loss.backward()
-            acc += loss.item()
-        opt.step()
-        losses.append(acc)
+
+    def train(model, dtype):
+        # ref train.py:190 casts the model to the run dtype; the loss is F.cross_entropy on the
+        # model's logits (ref train.py:46-49) in that dtype
+        model.to(dtype)
+        opt = torch.optim.AdamW(model.parameters(), lr=1e-3)
+        losses, k = [], 0
+        for step in range(steps):
+            opt.zero_grad()
+            acc = 0.0
+            for _ in range(grad_acc):
+                toks = batches[k % len(batches)]
+                k += 1
+                logits = model(input_ids=toks[:, :-1])
+                loss = torch.nn.functional.cross_entropy(logits.reshape(-1, V), toks[:, 1:].reshape(-1),
+                                                         reduction="mean") / grad_acc
+                loss.backward()
+                acc += loss.item()
+            opt.step()
+            losses.append(acc)
+        return losses
+
+    losses = train(model, torch.float32)
+    # the reference's bf16 dtype policy (its GPU path: bf16 params, bf16 AdamW states), same init
+    model.load_state_dict(init)
+    losses_bf16 = train(model, torch.bfloat16)
     fp = {k_: {"sum": float(v.double().sum()), "abs_sum": float(v.double().abs().sum()),
                "head": [float(x) for x in v.flatten()[:16]]} for k_, v in init.items()}
     with open(os.path.join(OUT, "tiny_init_fingerprint.json"), "w") as f:
         json.dump(fp, f)
     with open(os.path.join(OUT, "loss_curve_tiny.json"), "w") as f:
         json.dump({"config": TINY, "mbs": mbs, "seq": seq, "grad_acc": grad_acc, "lr": 1e-3, "seed": 42,
-                   "data": "arith, torch.Generator seed 1234, 16 cycled micro-batches", "losses": losses}, f)
-    print(f"loss curve: step0 {losses[0]:.5f} (ln V = {math.log(V):.5f}) -> step{steps - 1} {losses[-1]:.5f}")
+                   "data": "arith, torch.Generator seed 1234, 16 cycled micro-batches", "losses": losses,
+                   "losses_bf16": losses_bf16}, f)
+    print(f"loss curve: step0 {losses[0]:.5f} (ln V = {math.log(V):.5f}) -> step{steps - 1} {losses[-1]:.5f}; "
+          f"bf16 {losses_bf16[0]:.5f} -> {losses_bf16[-1]:.5f}")
     pgm.process_group_manager = None
 
 

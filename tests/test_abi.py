@@ -1,0 +1,86 @@
+"""The C-ABI library builds, loads without a GPU, exports every symbol include/picotron_hip.h
+declares, and rejects bad arguments with a status + message (no compute calls: CPU only)."""
+import ctypes
+import os
+import re
+
+import pytest
+import torch
+
+from conftest import ROOT
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from picotron_amd import _lib
+    if not os.path.exists(_lib.LIB_PATH):
+        from picotron_amd.build import build
+        build()
+    return _lib.load()
+
+
+def _declared():
+    src = open(os.path.join(ROOT, "include", "picotron_hip.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(pico_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_exports_every_declared_symbol(lib):
+    from picotron_amd import _lib
+    names = _declared()
+    assert len(names) >= 17
+    for n in names:
+        assert hasattr(lib, n), n
+        assert n in _lib.EXPORTED_SYMBOLS, f"{n} has no ctypes signature"
+    assert lib.pico_abi_version() == 1
+
+
+def test_struct_layout_matches(lib):
+    from picotron_amd import _lib
+    assert lib.pico_attn_args_size() == ctypes.sizeof(_lib.AttnArgs)
+
+
+def test_argument_errors_return_status(lib):
+    from picotron_amd import _lib
+    rc = lib.pico_rmsnorm_fwd(None, None, None, None, None, None, 4, 64, 1e-5, None)
+    assert rc == 1000 and b"null" in lib.pico_last_error()
+    rc = lib.pico_rmsnorm_fwd(ctypes.c_void_p(16), None, ctypes.c_void_p(16), ctypes.c_void_p(16), None,
+                              ctypes.c_void_p(16), 4, 12, 1e-5, None)
+    assert rc == 1000 and b"multiple of 8" in lib.pico_last_error()
+    a = _lib.AttnArgs()
+    a.q = a.k = a.v = ctypes.c_void_p(64)
+    a.batch, a.seqlen_q, a.seqlen_k, a.heads_q, a.heads_kv, a.head_dim = 1, 8, 8, 2, 2, 96
+    assert lib.pico_attn_fwd(ctypes.byref(a), None) == 1000
+    assert b"head_dim" in lib.pico_last_error()
+    a.head_dim, a.heads_kv = 64, 3
+    assert lib.pico_attn_fwd(ctypes.byref(a), None) == 1000
+    a.heads_kv, a.causal, a.seqlen_k = 2, 1, 9
+    assert lib.pico_attn_fwd(ctypes.byref(a), None) == 1000
+    assert b"causal" in lib.pico_last_error()
+    assert lib.pico_grad_accum(None, None, 10, 1.0, None) == 1000
+    assert lib.pico_prof_collect(7, ctypes.byref(ctypes.c_double()), ctypes.byref(ctypes.c_int64())) == 1000
+
+
+def test_workspace_sizes(lib):
+    assert lib.pico_rmsnorm_bwd_workspace_bytes(4096, 2048) == 256 * 2048 * 4
+    assert lib.pico_rmsnorm_bwd_workspace_bytes(3, 2048) == 1 * 2048 * 4
+    from picotron_amd import _lib
+    a = _lib.AttnArgs()
+    a.batch, a.seqlen_q, a.seqlen_k, a.heads_q, a.head_dim = 4, 1024, 1024, 32, 64
+    # delta + one fp32 dQ partial slab per 256-key block
+    assert lib.pico_attn_bwd_workspace_bytes(ctypes.byref(a)) == 4 * 32 * 1024 * 4 + 4 * (4 * 1024 * 32 * 64 * 4)
+
+
+def test_ops_fail_loudly_without_hip_tensors(lib):
+    from picotron_amd import ops
+    x = torch.randn(2, 8, 2, 64, dtype=torch.bfloat16)
+    with pytest.raises(RuntimeError):
+        ops.flash_attn_func(x, x, x, causal=True)
+    with pytest.raises(RuntimeError):
+        ops.rms_norm(torch.randn(4, 64, dtype=torch.bfloat16), torch.ones(64, dtype=torch.bfloat16))
+    with pytest.raises(RuntimeError):
+        ops.swiglu(torch.randn(8, dtype=torch.bfloat16), torch.randn(8, dtype=torch.bfloat16))
+    with pytest.raises(NotImplementedError):
+        ops.flash_attn_func(x, x, x, dropout_p=0.1)
+    with pytest.raises(NotImplementedError):
+        ops.layer_norm_fn(x, None, None, is_rms_norm=False)

@@ -1,0 +1,117 @@
+"""Multi-process (world size 2, gloo, CPU) tests of the data-parallel host path:
+picotron_amd's DataParallelBucket / BucketManager with the oracle's CPU device-op table, on the
+oracle Llama, against the reference's own DataParallelBucket run (tests/golden/dp_w2_tiny.safetensors).
+"""
+import os
+import socket
+from types import SimpleNamespace
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import GOLDEN, ROOT
+
+TINY_DP = dict(hidden_size=128, intermediate_size=256, num_attention_heads=2, num_key_value_heads=1,
+               num_hidden_layers=2, vocab_size=256, max_position_embeddings=64, rms_norm_eps=1e-5, rope_theta=10000.0)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, mode, outdir):
+    import sys
+    sys.path.insert(0, ROOT)
+    torch.set_num_threads(1)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from safetensors.torch import load_file, save_file
+    from oracle import hotpath as H
+    from oracle import model as OM
+    from picotron_amd import process_group_manager as pgm
+    from picotron_amd.data import synth_tokens
+    from picotron_amd.data_parallel import bucket as B
+    from picotron_amd.data_parallel.data_parallel import DataParallelBucket
+    pgm.setup_process_group_manager(tp_size=1, cp_size=1, pp_size=1, dp_size=world)
+    B.set_kernels(H.CpuBucketKernels())
+    cfg = SimpleNamespace(**TINY_DP)
+    model = OM.Llama(cfg)
+    gold = load_file(os.path.join(GOLDEN, "dp_w2_tiny.safetensors"))
+    model.load_state_dict({k[5:]: v for k, v in gold.items() if k.startswith("init.")}, strict=True)
+    ddp = DataParallelBucket(model, bucket_cap_mb=0.05)
+    out = {}
+    if mode == "golden":
+        gen = torch.Generator().manual_seed(7 + rank)
+        ga = 3
+        for i in range(ga):
+            toks = synth_tokens(2, cfg.max_position_embeddings + 1, cfg.vocab_size, gen, "arith")
+            ddp.require_backward_grad_sync = i == ga - 1
+            logits = ddp(input_ids=toks[:, :-1])
+            loss = torch.nn.functional.cross_entropy(logits.reshape(-1, cfg.vocab_size), toks[:, 1:].reshape(-1)) / ga
+            loss.backward()
+        for n, p in model.named_parameters():
+            out["main_grad." + n] = p.main_grad.clone()
+            out["grad." + n] = p.grad.clone()
+    elif mode == "semantics":
+        gen = torch.Generator().manual_seed(11 + rank)
+        toks = synth_tokens(2, cfg.max_position_embeddings + 1, cfg.vocab_size, gen, "arith")
+        # no_sync: accumulate only, no bucket fires, no .grad handed out
+        with ddp.no_sync():
+            ddp(input_ids=toks[:, :-1]).float().mean().backward()
+        assert all(b.handle is None for b in ddp.bucket_manager.buckets)
+        assert all(p.grad is None for p in model.parameters())
+        local = {n: p.main_grad.clone() for n, p in model.named_parameters()}
+        # syncing backward: every bucket fires once; main_grad = (local + g) / W summed over ranks
+        ddp(input_ids=toks[:, :-1]).float().mean().backward()
+        assert all(b.handle is not None for b in ddp.bucket_manager.buckets)
+        for n, p in model.named_parameters():
+            out["main_grad." + n] = p.main_grad.clone()
+            out["local." + n] = local[n]
+            assert torch.equal(p.grad, p.main_grad.to(p.dtype))
+        # reset zeroes every bucket and clears readiness
+        ddp.reset()
+        assert all(float(b.grad_data.abs().sum()) == 0 and not b.params_with_grad_ready
+                   for b in ddp.bucket_manager.buckets)
+        assert all(float(p.main_grad.abs().sum()) == 0 for p in model.parameters())
+    save_file({k: v.contiguous() for k, v in out.items()}, os.path.join(outdir, f"rank{rank}.safetensors"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _run(mode, tmp_path):
+    mp.start_processes(_worker, args=(2, _free_port(), mode, str(tmp_path)), nprocs=2, join=True,
+                       start_method="spawn")
+    from safetensors.torch import load_file
+    return [load_file(os.path.join(tmp_path, f"rank{r}.safetensors")) for r in range(2)]
+
+
+def test_dp_bucket_matches_reference_golden(tmp_path):
+    from safetensors.torch import load_file
+    gold = load_file(os.path.join(GOLDEN, "dp_w2_tiny.safetensors"))
+    r0, r1 = _run("golden", tmp_path)
+    n = 0
+    for k, v in gold.items():
+        if not k.startswith("main_grad."):
+            continue
+        name = k[len("main_grad."):]
+        # both ranks hold the same averaged gradient
+        assert torch.equal(r0[k], r1[k]), name
+        assert torch.allclose(r0[k], v, rtol=1e-5, atol=1e-7), (name, float((r0[k] - v).abs().max()))
+        assert torch.equal(r0["grad." + name], r0[k])  # fp32 params: .grad == main_grad
+        n += 1
+    assert n == 21
+
+
+def test_dp_sync_semantics(tmp_path):
+    r0, r1 = _run("semantics", tmp_path)
+    for k in r0:
+        if k.startswith("main_grad."):
+            name = k[len("main_grad."):]
+            assert torch.equal(r0[k], r1[k]), name
+            assert float(r0["local." + name].abs().sum()) > 0

@@ -106,13 +106,13 @@ def test_rope_golden(golden_kernels):
     assert rel_l2(q.grad.cpu(), g["rope.dx_f64"].transpose(1, 2)) < 4e-3
 
 
-@pytest.mark.parametrize("B,S,H,D", [(4, 1024, 32, 64), (1, 100, 3, 128), (2, 37, 8, 64)])
-def test_rope_shapes_and_strides(B, S, H, D):
+@pytest.mark.parametrize("B,S,NH,D", [(4, 1024, 32, 64), (1, 100, 3, 128), (2, 37, 8, 64)])
+def test_rope_shapes_and_strides(B, S, NH, D):
     ops = _ops()
     torch.manual_seed(S)
     cos, sin = H.get_cos_sin(S, D, base=10000.0)
-    big = torch.randn(B, S, H + 2, D, dtype=BF, device=DEV)
-    x = big[:, :, 1:H + 1]  # non-contiguous head slice (row stride (H+2)*D)
+    big = torch.randn(B, S, NH + 2, D, dtype=BF, device=DEV)
+    x = big[:, :, 1:NH + 1]  # non-contiguous head slice (row stride (NH+2)*D)
     out = ops.apply_rotary_emb(x, cos.to(DEV)[:, : D // 2], sin.to(DEV)[:, : D // 2])
     ref = H.rope_fused(x.cpu().double(), cos.double(), sin.double())
     assert rel_l2(out.cpu(), ref) < 4e-3
@@ -291,10 +291,13 @@ def test_grad_accum_and_cast_bit_exact():
         ref = m.clone().add_(g)
         K.accumulate(m, g, 1)
         assert torch.equal(m, ref)
-        ref = (m.clone().add_(g)) / 8
-        K.accumulate(m, g, 8)
-        assert torch.equal(m, ref)
-        ref = m.clone() / 3
+        for W in (8, 3, 6):  # reference: add_ then /= W (ATen: * fp32(1/W) on the GPU)
+            ref = m.clone().add_(g)
+            ref /= W
+            K.accumulate(m, g, W)
+            assert torch.equal(m, ref), W
+        ref = m.clone()
+        ref /= 3
         K.scale(m, 3)
         assert torch.equal(m, ref)
         out = torch.empty(n, dtype=BF, device=DEV)

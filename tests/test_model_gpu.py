@@ -63,24 +63,29 @@ def _loss_curve(model, golden_loss, steps, fused=False):
 
 
 def test_loss_curve_overlays_reference(golden_loss):
-    """200 steps, bf16 params + bf16 AdamW states (the reference's GPU dtype policy, ref train.py:76,190)
-    vs the reference's fp32 CPU curve. Tolerance: step 0 == ln V to 1e-3; after step 10
-    |dloss| <= 0.05 + 5 % of the reference loss; mean |dloss| <= 0.03."""
+    """200 steps with bf16 params + bf16 AdamW states (the reference's GPU dtype policy, ref
+    train.py:76,190) against the reference's own run of the same init/data in that dtype policy
+    (its eager path on CPU, `losses_bf16`). Tolerance: step 0 == ln V to 1e-3 (zero LM head);
+    after step 10 |dloss| <= 0.06 + 3 % of the reference loss (the reference's loss values are
+    bf16-rounded: 1 ulp = 0.8 %); mean |dloss| <= 0.02. Against the fp32 curve the bf16 policy
+    itself lags by up to ~0.25 (recorded, loosely bounded)."""
     from picotron_amd.model import build_llama
     torch.manual_seed(golden_loss["seed"])
     m = build_llama(_cfg(golden_loss), device="cuda", dtype=BF)
     losses = _loss_curve(m, golden_loss, 200)
-    ref = golden_loss["losses"]
+    ref = golden_loss["losses_bf16"]
+    ref32 = golden_loss["losses"]
     out = os.environ.get("PICO_LOSS_OUT")
     if out:
         import json
         with open(out, "w") as f:
-            json.dump({"gpu_bf16": losses, "reference_cpu_fp32": ref}, f)
+            json.dump({"gpu_bf16": losses, "reference_cpu_bf16": ref, "reference_cpu_fp32": ref32}, f)
     assert abs(losses[0] - math.log(golden_loss["config"]["vocab_size"])) < 1e-3
     diffs = [abs(a - b) for a, b in zip(losses, ref)]
     for i in range(10, 200):
-        assert diffs[i] <= 0.05 + 0.05 * ref[i], (i, losses[i], ref[i])
-    assert sum(diffs) / len(diffs) <= 0.03
+        assert diffs[i] <= 0.06 + 0.03 * ref[i], (i, losses[i], ref[i])
+    assert sum(diffs) / len(diffs) <= 0.02
+    assert sum(abs(a - b) for a, b in zip(losses, ref32)) / 200 <= 0.25
 
 
 def test_dp_bucket_rccl_world1(golden_loss):
@@ -100,8 +105,11 @@ def test_dp_bucket_rccl_world1(golden_loss):
         model = build_llama(cfg, "cuda", BF)
         # capture hooks registered BEFORE the DP hooks see each micro-batch's raw bf16 grad
         grads = {p: torch.zeros_like(p, dtype=torch.float32) for p in model.parameters()}
+        def capture(q):
+            grads[q].add_(q.grad.float())
+
         for p in model.parameters():
-            p.register_post_accumulate_grad_hook(lambda q: grads[q].add_(q.grad.float()))
+            p.register_post_accumulate_grad_hook(capture)
         ddp = DataParallelBucket(model, bucket_cap_mb=1)
         assert len(ddp.bucket_manager.buckets) > 1
         torch.manual_seed(5)
