@@ -43,14 +43,17 @@ def kernel_work(kid, cfg, mbs, seq):
     from picotron_amd import _lib as L
     T = mbs * seq
     Hd, I, H = cfg.hidden_size, cfg.intermediate_size, cfg.num_attention_heads
+    Hkv = cfg.num_key_value_heads
     D = Hd // H
     attn_fwd = 4.0 * mbs * H * seq * seq * D / 2  # causal
     table = {
         L.K_ATTN_FWD: (attn_fwd, "flop", "mfma"),
         L.K_ATTN_BWD: (2.5 * attn_fwd, "flop", "mfma"),
-        L.K_RMSNORM_FWD: (2 * T * Hd * 2 + 4 * T, "byte", "hbm"),
-        L.K_RMSNORM_BWD: (3 * T * Hd * 2 + 4 * T, "byte", "hbm"),
-        L.K_ROPE: (2 * T * Hd * 2, "byte", "hbm"),  # one of q / k per launch (Hq = Hkv)
+        # residual-fused form (29 of 31 launches): fwd reads x, residual, writes y, residual_out;
+        # bwd reads dy, d(residual_out), x, writes dx (+4 B/row rstd, small dw partials)
+        L.K_RMSNORM_FWD: (4 * T * Hd * 2 + 4 * T, "byte", "hbm"),
+        L.K_RMSNORM_BWD: (4 * T * Hd * 2 + 4 * T, "byte", "hbm"),
+        L.K_ROPE: (2 * T * (H + Hkv) * D * 2, "byte", "hbm"),  # q|k heads in one launch, read + write
         L.K_SWIGLU_FWD: (3 * T * I * 2, "byte", "hbm"),
         L.K_SWIGLU_BWD: (5 * T * I * 2, "byte", "hbm"),
         L.K_ATTN_BWD_PRE: (2 * T * Hd * 2 + T * H * 4 + T * Hd * 4, "byte", "hbm"),
@@ -60,6 +63,10 @@ def kernel_work(kid, cfg, mbs, seq):
 
 
 def main():
+    # Keep stdout for the ONE JSON line: native libraries (RCCL prints a banner at communicator
+    # creation) write to fd 1, so point fd 1 at stderr and write the result to the saved fd.
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
@@ -212,7 +219,7 @@ def main():
             "kernels": kernels,
             "cpu_baseline": cpu_baseline,
         }
-        print(json.dumps(out), flush=True)
+        os.write(json_fd, (json.dumps(out) + "\n").encode())
     dist.barrier()
     dist.destroy_process_group()
 

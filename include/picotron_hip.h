@@ -93,10 +93,13 @@ int pico_rope(const void* x, void* out, const void* cos, const void* sin, int64_
               int64_t seqlen, int64_t heads, int64_t head_dim, const int64_t* x_strides,
               const int64_t* out_strides, int64_t cs_stride, int conjugate, void* stream);
 
-/* ---- SwiGLU epilogue: h = silu(g) * u over n contiguous bf16 elements ---- */
-int pico_swiglu_fwd(const void* gate, const void* up, void* out, int64_t n, void* stream);
+/* ---- SwiGLU epilogue: h = silu(g) * u on [rows, cols] bf16 ----
+ * gate/up (and dgate/dup) rows at element stride in_stride (they may be the two column halves of one
+ * fused gate|up GEMM output, in_stride = 2*cols); out/dout rows at out_stride. */
+int pico_swiglu_fwd(const void* gate, const void* up, void* out, int64_t rows, int64_t cols,
+                    int64_t in_stride, int64_t out_stride, void* stream);
 int pico_swiglu_bwd(const void* dout, const void* gate, const void* up, void* dgate, void* dup,
-                    int64_t n, void* stream);
+                    int64_t rows, int64_t cols, int64_t in_stride, int64_t out_stride, void* stream);
 
 /* ---- Flash attention (bf16 MFMA, online softmax, fp32 LSE) ----
  * Layouts: q/o/do/dq [B, Sq, Hq, D], k/v/dk/dv [B, Sk, Hkv, D] with element strides

@@ -2,36 +2,15 @@
 //
 // Replaces the two ATen kernels of F.silu(self.gate_proj(x)) * self.up_proj(x)
 // (ref picotron/model.py:183-185) and their autograd backward. fp32 math, one rounding per output.
-// 8 bf16 per thread per tensor (16-byte loads/stores), grid-stride.
+// 8 bf16 per thread per tensor (16-byte loads/stores), grid-stride; gate and up may be the two
+// column halves of one fused gate|up GEMM output (row stride 2*I), and the backward writes dgate/dup
+// straight into the two halves of the fused GEMM's input gradient.
 // Algorithmic bytes per element: fwd 3 * 2 B, bwd 5 * 2 B.
 #include "common.h"
 
 namespace {
 
 PICO_DEV float sigmoidf_(float g) { return 1.f / (1.f + __expf(-g)); }
-
-__global__ __launch_bounds__(256) void swiglu_fwd_kernel(const bf16_t* __restrict__ g, const bf16_t* __restrict__ u,
-                                                         bf16_t* __restrict__ h, int64_t n) {
-  const int64_t nv = n / 8;
-  const int64_t stride = (int64_t)gridDim.x * 256;
-  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < nv; t += stride) {
-    const u16x8 gv = reinterpret_cast<const u16x8*>(g)[t];
-    const u16x8 uv = reinterpret_cast<const u16x8*>(u)[t];
-    u16x8 o;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float gf = bf2f(gv[j]);
-      o[j] = f2bf(gf * sigmoidf_(gf) * bf2f(uv[j]));
-    }
-    reinterpret_cast<u16x8*>(h)[t] = o;
-  }
-  // scalar tail (n % 8 elements), handled by the first threads of block 0
-  if (blockIdx.x == 0 && threadIdx.x < (n & 7)) {
-    const int64_t i = nv * 8 + threadIdx.x;
-    const float gf = bf2f(g[i]);
-    h[i] = f2bf(gf * sigmoidf_(gf) * bf2f(u[i]));
-  }
-}
 
 PICO_DEV void swiglu_grad(float dh, float gf, float uf, float& dg, float& du) {
   const float sg = sigmoidf_(gf);
@@ -40,15 +19,43 @@ PICO_DEV void swiglu_grad(float dh, float gf, float uf, float& dg, float& du) {
   dg = dh * uf * sg * (1.f + gf * (1.f - sg));
 }
 
+// 2-D strided form: gate/up rows of `cols` elements at row stride `in_stride` (gate and up may be
+// the two column halves of one fused [rows, 2*cols] GEMM output), out rows at `out_stride`.
+// Vector path: 8 elements (16 B) per thread; requires cols, strides % 8 == 0 and 16-B alignment.
+__global__ __launch_bounds__(256) void swiglu_fwd_kernel(const bf16_t* __restrict__ g, const bf16_t* __restrict__ u,
+                                                         bf16_t* __restrict__ h, int64_t rows, int cols, int64_t is,
+                                                         int64_t os) {
+  const unsigned vpr = (unsigned)cols / 8;
+  const unsigned nv = (unsigned)(rows * vpr);  // host guarantees < 2^31
+  for (unsigned t = blockIdx.x * 256 + threadIdx.x; t < nv; t += gridDim.x * 256) {
+    const unsigned row32 = t / vpr;
+    const int64_t row = row32;
+    const int c = (int)(t - row32 * vpr) * 8;
+    const u16x8 gv = *reinterpret_cast<const u16x8*>(g + row * is + c);
+    const u16x8 uv = *reinterpret_cast<const u16x8*>(u + row * is + c);
+    u16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float gf = bf2f(gv[j]);
+      o[j] = f2bf(gf * sigmoidf_(gf) * bf2f(uv[j]));
+    }
+    *reinterpret_cast<u16x8*>(h + row * os + c) = o;
+  }
+}
+
 __global__ __launch_bounds__(256) void swiglu_bwd_kernel(const bf16_t* __restrict__ dh, const bf16_t* __restrict__ g,
                                                          const bf16_t* __restrict__ u, bf16_t* __restrict__ dg,
-                                                         bf16_t* __restrict__ du, int64_t n) {
-  const int64_t nv = n / 8;
-  const int64_t stride = (int64_t)gridDim.x * 256;
-  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < nv; t += stride) {
-    const u16x8 dv = reinterpret_cast<const u16x8*>(dh)[t];
-    const u16x8 gv = reinterpret_cast<const u16x8*>(g)[t];
-    const u16x8 uv = reinterpret_cast<const u16x8*>(u)[t];
+                                                         bf16_t* __restrict__ du, int64_t rows, int cols, int64_t is,
+                                                         int64_t os) {
+  const unsigned vpr = (unsigned)cols / 8;
+  const unsigned nv = (unsigned)(rows * vpr);  // host guarantees < 2^31
+  for (unsigned t = blockIdx.x * 256 + threadIdx.x; t < nv; t += gridDim.x * 256) {
+    const unsigned row32 = t / vpr;
+    const int64_t row = row32;
+    const int c = (int)(t - row32 * vpr) * 8;
+    const u16x8 dv = *reinterpret_cast<const u16x8*>(dh + row * os + c);
+    const u16x8 gv = *reinterpret_cast<const u16x8*>(g + row * is + c);
+    const u16x8 uv = *reinterpret_cast<const u16x8*>(u + row * is + c);
     u16x8 og, ou;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -57,50 +64,98 @@ __global__ __launch_bounds__(256) void swiglu_bwd_kernel(const bf16_t* __restric
       og[j] = f2bf(a);
       ou[j] = f2bf(b);
     }
-    reinterpret_cast<u16x8*>(dg)[t] = og;
-    reinterpret_cast<u16x8*>(du)[t] = ou;
-  }
-  if (blockIdx.x == 0 && threadIdx.x < (n & 7)) {
-    const int64_t i = nv * 8 + threadIdx.x;
-    float a, b;
-    swiglu_grad(bf2f(dh[i]), bf2f(g[i]), bf2f(u[i]), a, b);
-    dg[i] = f2bf(a);
-    du[i] = f2bf(b);
+    *reinterpret_cast<u16x8*>(dg + row * is + c) = og;
+    *reinterpret_cast<u16x8*>(du + row * is + c) = ou;
   }
 }
 
-int grid_for(int64_t n) {
-  int64_t nb = (n / 8 + 255) / 256;
+// scalar fallback (unaligned / ragged shapes)
+__global__ __launch_bounds__(256) void swiglu_fwd_scalar(const bf16_t* __restrict__ g, const bf16_t* __restrict__ u,
+                                                         bf16_t* __restrict__ h, int64_t rows, int cols, int64_t is,
+                                                         int64_t os) {
+  const int64_t n = rows * cols;
+  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < n; t += (int64_t)gridDim.x * 256) {
+    const int64_t row = t / cols;
+    const int c = (int)(t - row * cols);
+    const float gf = bf2f(g[row * is + c]);
+    h[row * os + c] = f2bf(gf * sigmoidf_(gf) * bf2f(u[row * is + c]));
+  }
+}
+
+__global__ __launch_bounds__(256) void swiglu_bwd_scalar(const bf16_t* __restrict__ dh, const bf16_t* __restrict__ g,
+                                                         const bf16_t* __restrict__ u, bf16_t* __restrict__ dg,
+                                                         bf16_t* __restrict__ du, int64_t rows, int cols, int64_t is,
+                                                         int64_t os) {
+  const int64_t n = rows * cols;
+  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < n; t += (int64_t)gridDim.x * 256) {
+    const int64_t row = t / cols;
+    const int c = (int)(t - row * cols);
+    float a, b;
+    swiglu_grad(bf2f(dh[row * os + c]), bf2f(g[row * is + c]), bf2f(u[row * is + c]), a, b);
+    dg[row * is + c] = f2bf(a);
+    du[row * is + c] = f2bf(b);
+  }
+}
+
+int grid_for(int64_t work) {
+  int64_t nb = (work + 255) / 256;
   if (nb < 1) nb = 1;
   if (nb > 4096) nb = 4096;  // 256 CUs x 16 workgroups, grid-stride beyond
   return (int)nb;
+}
+
+bool vec_ok(int64_t cols, int64_t is, int64_t os, const void* a, const void* b, const void* c) {
+  return cols % 8 == 0 && is % 8 == 0 && os % 8 == 0 && ((uintptr_t)a | (uintptr_t)b | (uintptr_t)c) % 16 == 0;
 }
 
 }  // namespace
 
 extern "C" {
 
-int pico_swiglu_fwd(const void* gate, const void* up, void* out, int64_t n, void* stream) {
+int pico_swiglu_fwd(const void* gate, const void* up, void* out, int64_t rows, int64_t cols, int64_t in_stride,
+                    int64_t out_stride, void* stream) {
   PICO_REQUIRE(gate && up && out, "pico_swiglu_fwd: null pointer");
-  PICO_REQUIRE(((uintptr_t)gate | (uintptr_t)up | (uintptr_t)out) % 16 == 0,
-               "pico_swiglu_fwd: pointers must be 16-byte aligned");
-  if (n <= 0) return 0;
+  PICO_REQUIRE(rows >= 0 && cols >= 0 && cols < (1ll << 31) && in_stride >= cols && out_stride >= cols,
+               "pico_swiglu_fwd: bad shape");
+  if (rows * cols == 0) return 0;
+  PICO_REQUIRE(rows * cols < (1ll << 31), "pico_swiglu_fwd: tensor too large");
   hipStream_t s = (hipStream_t)stream;
-  PICO_LAUNCH(PICO_K_SWIGLU_FWD, "swiglu_fwd", s,
-              swiglu_fwd_kernel<<<grid_for(n), 256, 0, s>>>((const bf16_t*)gate, (const bf16_t*)up, (bf16_t*)out, n));
+  auto g = (const bf16_t*)gate;
+  auto u = (const bf16_t*)up;
+  auto h = (bf16_t*)out;
+  if (vec_ok(cols, in_stride, out_stride, gate, up, out)) {
+    PICO_LAUNCH(PICO_K_SWIGLU_FWD, "swiglu_fwd", s,
+                swiglu_fwd_kernel<<<grid_for(rows * cols / 8), 256, 0, s>>>(g, u, h, rows, (int)cols, in_stride,
+                                                                             out_stride));
+  } else {
+    PICO_LAUNCH(PICO_K_SWIGLU_FWD, "swiglu_fwd", s,
+                swiglu_fwd_scalar<<<grid_for(rows * cols), 256, 0, s>>>(g, u, h, rows, (int)cols, in_stride,
+                                                                        out_stride));
+  }
   return 0;
 }
 
-int pico_swiglu_bwd(const void* dout, const void* gate, const void* up, void* dgate, void* dup, int64_t n,
-                    void* stream) {
+int pico_swiglu_bwd(const void* dout, const void* gate, const void* up, void* dgate, void* dup, int64_t rows,
+                    int64_t cols, int64_t in_stride, int64_t out_stride, void* stream) {
   PICO_REQUIRE(dout && gate && up && dgate && dup, "pico_swiglu_bwd: null pointer");
-  PICO_REQUIRE(((uintptr_t)dout | (uintptr_t)gate | (uintptr_t)up | (uintptr_t)dgate | (uintptr_t)dup) % 16 == 0,
-               "pico_swiglu_bwd: pointers must be 16-byte aligned");
-  if (n <= 0) return 0;
+  PICO_REQUIRE(rows >= 0 && cols >= 0 && cols < (1ll << 31) && in_stride >= cols && out_stride >= cols,
+               "pico_swiglu_bwd: bad shape");
+  if (rows * cols == 0) return 0;
+  PICO_REQUIRE(rows * cols < (1ll << 31), "pico_swiglu_bwd: tensor too large");
   hipStream_t s = (hipStream_t)stream;
-  PICO_LAUNCH(PICO_K_SWIGLU_BWD, "swiglu_bwd", s,
-              swiglu_bwd_kernel<<<grid_for(n), 256, 0, s>>>((const bf16_t*)dout, (const bf16_t*)gate,
-                                                            (const bf16_t*)up, (bf16_t*)dgate, (bf16_t*)dup, n));
+  const bool vec = vec_ok(cols, in_stride, out_stride, dout, gate, up) &&
+                   ((uintptr_t)dgate | (uintptr_t)dup) % 16 == 0;
+  if (vec) {
+    PICO_LAUNCH(PICO_K_SWIGLU_BWD, "swiglu_bwd", s,
+                swiglu_bwd_kernel<<<grid_for(rows * cols / 8), 256, 0, s>>>(
+                    (const bf16_t*)dout, (const bf16_t*)gate, (const bf16_t*)up, (bf16_t*)dgate, (bf16_t*)dup, rows,
+                    (int)cols, in_stride, out_stride));
+  } else {
+    PICO_LAUNCH(PICO_K_SWIGLU_BWD, "swiglu_bwd", s,
+                swiglu_bwd_scalar<<<grid_for(rows * cols), 256, 0, s>>>(
+                    (const bf16_t*)dout, (const bf16_t*)gate, (const bf16_t*)up, (bf16_t*)dgate, (bf16_t*)dup, rows,
+                    (int)cols, in_stride, out_stride));
+  }
   return 0;
 }
 

@@ -137,9 +137,20 @@ class Attention(nn.Module):
             bound = math.sqrt(1 / w.size(1))
             torch.nn.init.uniform_(w, -bound, bound)
 
+    def _fusable(self):
+        return (os.getenv("CONTEXT_PARALLEL", "0") != "1" and os.getenv("PICO_UNFUSED", "0") != "1"
+                and all(type(m) is nn.Linear and m.bias is None for m in (self.q_proj, self.k_proj, self.v_proj)))
+
     def forward(self, x, cos, sin, attention_mask=None, position_ids=None):
         B, S, _ = x.size()
         D = self.head_dim
+        if self._fusable():
+            # one q|k|v GEMM, RoPE in place on q|k, attention on strided views (ops._QKVRopeAttentionFn)
+            if not hasattr(self, "_wcache"):
+                self._wcache = ops._CatCache()
+            out = ops.qkv_rope_attention(x, self.q_proj.weight, self.k_proj.weight, self.v_proj.weight, cos, sin,
+                                         self.num_local_heads, self.num_local_kv_heads, True, self._wcache)
+            return self.out_proj(out)
         q = self.q_proj(x).view(B, S, self.num_local_heads, D)
         k = self.k_proj(x).view(B, S, self.num_local_kv_heads, D)
         v = self.v_proj(x).view(B, S, self.num_local_kv_heads, D)
@@ -171,6 +182,12 @@ class MLP(nn.Module):
             torch.nn.init.uniform_(w, -bound, bound)
 
     def forward(self, x):
+        if (os.getenv("PICO_UNFUSED", "0") != "1" and type(self.gate_proj) is nn.Linear
+                and type(self.up_proj) is nn.Linear and self.gate_proj.bias is None and self.up_proj.bias is None):
+            # one gate|up GEMM + strided SwiGLU (ops._GateUpSwiGLUFn)
+            if not hasattr(self, "_wcache"):
+                self._wcache = ops._CatCache()
+            return self.down_proj(ops.gate_up_swiglu(x, self.gate_proj.weight, self.up_proj.weight, self._wcache))
         return self.down_proj(ops.swiglu(self.gate_proj(x), self.up_proj(x)))
 
 
@@ -194,6 +211,19 @@ class DecoderLayer(nn.Module):
         x = x + self.attention(self.input_layernorm(x), cos, sin, attention_mask, position_ids)
         x = x + self.mlp(self.post_attention_layernorm(x))
         return x
+
+    def forward_fused(self, delta, residual):
+        """Same layer with the residual adds fused into the norms (layer_norm_fn prenorm form):
+        the layer input is residual + delta (residual None for the first layer). Returns the
+        (delta, residual) pair whose sum is this layer's output; every sum is rounded to bf16 exactly
+        like the reference's `x + f(x)`."""
+        if residual is None:
+            h_in, x = self.input_layernorm(delta), delta
+        else:
+            h_in, x = self.input_layernorm(delta, residual=residual, prenorm=True)
+        attn = self.attention(h_in, self.cos, self.sin)
+        h2, x = self.post_attention_layernorm(attn, residual=x, prenorm=True)
+        return self.mlp(h2), x
 
 
 class Embedding(nn.Module):
@@ -249,10 +279,16 @@ class Llama(nn.Module):
 
     def forward(self, input_ids, attention_mask=None, position_ids: torch.Tensor = None):
         x = self.embedding(input_ids)
+        if os.getenv("PICO_UNFUSED", "0") == "1":
+            for layer in self.decoder_layers:
+                x = layer(x)
+            return self.final_proj(self.final_norm(x))
+        delta, residual = x, None
         for layer in self.decoder_layers:
-            x = layer(x)
-        x = self.final_norm(x)
-        return self.final_proj(x)
+            delta, residual = layer.forward_fused(delta, residual)
+        if residual is None:
+            return self.final_proj(self.final_norm(delta))
+        return self.final_proj(self.final_norm(delta, residual=residual))
 
 
 def build_llama(config, device="cuda", dtype=torch.bfloat16):

@@ -167,6 +167,16 @@ def apply_rotary_emb(x, cos, sin, interleaved=False, inplace=False, seqlen_offse
 # --------------------------------------------------------------------------------------------
 # SwiGLU epilogue
 # --------------------------------------------------------------------------------------------
+def _swiglu_fwd(g, u, out, rows, cols, in_stride, out_stride):
+    _lib.check(_lib.load().pico_swiglu_fwd(_lib.ptr(g), _lib.ptr(u), _lib.ptr(out), rows, cols, in_stride, out_stride,
+                                           _lib.stream_of(g)), "pico_swiglu_fwd")
+
+
+def _swiglu_bwd(dh, g, u, dg, du, rows, cols, in_stride, out_stride):
+    _lib.check(_lib.load().pico_swiglu_bwd(_lib.ptr(dh), _lib.ptr(g), _lib.ptr(u), _lib.ptr(dg), _lib.ptr(du), rows,
+                                           cols, in_stride, out_stride, _lib.stream_of(dh)), "pico_swiglu_bwd")
+
+
 class _SwiGLUFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, gate, up):
@@ -177,9 +187,8 @@ class _SwiGLUFn(torch.autograd.Function):
         g = gate.contiguous()
         u = up.contiguous()
         out = torch.empty_like(g)
-        lib = _lib.load()
-        _lib.check(lib.pico_swiglu_fwd(_lib.ptr(g), _lib.ptr(u), _lib.ptr(out), g.numel(), _lib.stream_of(g)),
-                   "pico_swiglu_fwd")
+        n = g.numel()
+        _swiglu_fwd(g, u, out, 1, n, n, n)
         ctx.save_for_backward(g, u)
         return out
 
@@ -189,15 +198,69 @@ class _SwiGLUFn(torch.autograd.Function):
         d = dout.contiguous()
         dg = torch.empty_like(g)
         du = torch.empty_like(u)
-        lib = _lib.load()
-        _lib.check(lib.pico_swiglu_bwd(_lib.ptr(d), _lib.ptr(g), _lib.ptr(u), _lib.ptr(dg), _lib.ptr(du), g.numel(),
-                                       _lib.stream_of(d)), "pico_swiglu_bwd")
+        n = g.numel()
+        _swiglu_bwd(d, g, u, dg, du, 1, n, n, n)
         return dg, du
 
 
 def swiglu(gate, up):
     """silu(gate) * up with one fused kernel each way (ref picotron/model.py:185)."""
     return _SwiGLUFn.apply(gate, up)
+
+
+# --------------------------------------------------------------------------------------------
+# Weight concatenation cache for the fused GEMMs: the concatenated weight is rebuilt only when one
+# of its parameters changed (optimizer step bumps the tensor version), i.e. once per training
+# step rather than once per micro-batch.
+# --------------------------------------------------------------------------------------------
+class _CatCache:
+    def __init__(self):
+        self.key = None
+        self.value = None
+
+    def get(self, ws):
+        key = tuple((w.data_ptr(), w._version, tuple(w.shape)) for w in ws)
+        if key != self.key:
+            with torch.no_grad():
+                self.value = torch.cat([w.detach() for w in ws], 0)
+            self.key = key
+        return self.value
+
+
+class _GateUpSwiGLUFn(torch.autograd.Function):
+    """h = silu(x Wg^T) * (x Wu^T) with ONE GEMM against [Wg; Wu] and the strided SwiGLU kernel on
+    its two column halves; the backward writes dgate/dup into the halves of one [T, 2I] gradient,
+    so x's gradient is one GEMM (no sum of two dgrads) and the weight gradient one GEMM."""
+
+    @staticmethod
+    def forward(ctx, x, w_gate, w_up, cache):
+        _need(x, "x")
+        I = w_gate.shape[0]
+        W = cache.get((w_gate, w_up))
+        x2 = x.reshape(-1, x.shape[-1])
+        gu = torch.matmul(x2, W.t())  # [T, 2I]
+        h = torch.empty((x2.shape[0], I), dtype=x.dtype, device=x.device)
+        _swiglu_fwd(gu, gu[:, I:], h, gu.shape[0], I, 2 * I, I)
+        ctx.save_for_backward(x2, gu, W)
+        ctx.xshape = x.shape
+        return h.view(*x.shape[:-1], I)
+
+    @staticmethod
+    def backward(ctx, dh):
+        x2, gu, W = ctx.saved_tensors
+        I = gu.shape[1] // 2
+        d = dh.reshape(-1, I)
+        if not d.is_contiguous():
+            d = d.contiguous()
+        dgu = torch.empty_like(gu)
+        _swiglu_bwd(d, gu, gu[:, I:], dgu, dgu[:, I:], gu.shape[0], I, 2 * I, I)
+        dx = torch.matmul(dgu, W).view(ctx.xshape)
+        dW = torch.matmul(dgu.t(), x2)
+        return dx, dW[:I], dW[I:], None
+
+
+def gate_up_swiglu(x, w_gate, w_up, cache):
+    return _GateUpSwiGLUFn.apply(x, w_gate, w_up, cache)
 
 
 # --------------------------------------------------------------------------------------------
@@ -305,3 +368,73 @@ def flash_attn_func(q, k, v, dropout_p=0.0, softmax_scale=None, causal=False, wi
     if softmax_scale is None:
         softmax_scale = 1.0 / math.sqrt(q.shape[-1])
     return _FlashAttnFn.apply(q, k, v, float(softmax_scale), bool(causal))
+
+
+class _QKVRopeAttentionFn(torch.autograd.Function):
+    """The attention block's hot path in one autograd node:
+      qkv = x [Wq; Wk; Wv]^T (ONE GEMM) -> RoPE in place on the q|k columns (ONE launch, q and k heads
+      are adjacent in qkv) -> flash attention reading q/k/v as strided views of qkv.
+    Backward: attention writes dq/dk/dv straight into the column blocks of one dqkv buffer, RoPE^-1
+    runs in place on dq|dk, then dx = dqkv W (one GEMM, no sum of three dgrads) and
+    dW = dqkv^T x (one GEMM, rows = dWq | dWk | dWv)."""
+
+    @staticmethod
+    def forward(ctx, x, wq, wk, wv, cos, sin, nh, nkv, causal, cache):
+        _need(x, "x")
+        B, S, Hd = x.shape
+        D = wq.shape[0] // nh
+        W = cache.get((wq, wk, wv))
+        N = W.shape[0]
+        x2 = x.reshape(B * S, Hd)
+        qkv = torch.matmul(x2, W.t())  # [T, (nh + 2 nkv) D]
+        qk = qkv.view(B, S, N // D, D)[:, :, : nh + nkv]  # q|k heads, row stride N
+        _rope_launch(qk, qk, cos, sin, False)
+        heads = qkv.view(B, S, N // D, D)
+        q, k, v = heads[:, :, :nh], heads[:, :, nh:nh + nkv], heads[:, :, nh + nkv:]
+        scale = 1.0 / math.sqrt(D)
+        o, lse = attention_block_fwd(q, k, v, scale, causal)
+        ctx.save_for_backward(x2, W, qkv, o, lse, cos, sin)
+        ctx.meta = (B, S, Hd, nh, nkv, D, causal, scale)
+        return o.view(B, S, nh * D)
+
+    @staticmethod
+    def backward(ctx, do):
+        x2, W, qkv, o, lse, cos, sin = ctx.saved_tensors
+        B, S, Hd, nh, nkv, D, causal, scale = ctx.meta
+        N = W.shape[0]
+        heads = qkv.view(B, S, N // D, D)
+        q, k, v = heads[:, :, :nh], heads[:, :, nh:nh + nkv], heads[:, :, nh + nkv:]
+        dqkv = torch.empty_like(qkv)
+        dheads = dqkv.view(B, S, N // D, D)
+        _attention_bwd_into(do.reshape(B, S, nh, D), q, k, v, o, lse, scale, causal,
+                            dheads[:, :, :nh], dheads[:, :, nh:nh + nkv], dheads[:, :, nh + nkv:])
+        dqk = dheads[:, :, : nh + nkv]
+        _rope_launch(dqk, dqk, cos, sin, True)
+        dx = torch.matmul(dqkv, W).view(B, S, Hd)
+        dW = torch.matmul(dqkv.t(), x2)
+        nq, nk = nh * D, nkv * D
+        return dx, dW[:nq], dW[nq:nq + nk], dW[nq + nk:], None, None, None, None, None, None
+
+
+def qkv_rope_attention(x, wq, wk, wv, cos, sin, num_heads, num_kv_heads, causal, cache):
+    """Fused attention block (projections + RoPE + flash attention); see _QKVRopeAttentionFn."""
+    D = wq.shape[0] // num_heads
+    return _QKVRopeAttentionFn.apply(x, wq, wk, wv, cos[:, : D // 2], sin[:, : D // 2], num_heads, num_kv_heads,
+                                     causal, cache)
+
+
+def _attention_bwd_into(dout, q, k, v, o, lse, softmax_scale, causal, dq, dk, dv):
+    """attention backward writing into caller-provided (possibly strided) dq/dk/dv."""
+    if dout.stride(-1) != 1 or any(s_ % 8 for s_ in dout.stride()[:3]):
+        dout = dout.contiguous()
+    a = _attn_args(q, k, v, o, lse, softmax_scale, causal)
+    a.dout = _lib.ptr(dout)
+    a.do_strides = _lib.i64x3(dout.stride()[:3])
+    a.dq, a.dk, a.dv = _lib.ptr(dq), _lib.ptr(dk), _lib.ptr(dv)
+    a.dq_strides = _lib.i64x3(dq.stride()[:3])
+    a.dk_strides = _lib.i64x3(dk.stride()[:3])
+    a.dv_strides = _lib.i64x3(dv.stride()[:3])
+    lib = _lib.load()
+    ws = torch.empty(lib.pico_attn_bwd_workspace_bytes(ctypes.byref(a)), dtype=torch.uint8, device=q.device)
+    a.workspace = _lib.ptr(ws)
+    _lib.check(lib.pico_attn_bwd(ctypes.byref(a), _lib.stream_of(q)), "pico_attn_bwd")

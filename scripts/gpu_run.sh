@@ -22,6 +22,9 @@ for s in $STAGES; do
     bench)
       timeout -k 10 900 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.json 2> gpurun_out/bench.log
       ok_or_stop $? bench ;;
+    attn)
+      timeout -k 10 300 python scripts/attn_bench.py --configs ${ATTN_CONFIGS:-c2,c2_full,d128,gqa4} > gpurun_out/attn_bench.jsonl 2> gpurun_out/attn_bench.log
+      ok_or_stop $? attn ;;
     gemm)
       timeout -k 10 300 python scripts/gemm_bench.py > gpurun_out/gemm_default.jsonl 2>&1
       ok_or_stop $? gemm_default

@@ -129,3 +129,27 @@ def test_dp_bucket_rccl_world1(golden_loss):
     finally:
         pgm.process_group_manager = None
         dist.destroy_process_group()
+
+
+def test_fused_paths_match_unfused(golden_loss, monkeypatch):
+    """Fused q|k|v GEMM + in-place RoPE + strided attention, fused gate|up GEMM + strided SwiGLU and
+    residual-add-in-RMSNorm give the same logits / grads as the module-by-module path (GEMM tiling
+    differs, so within bf16 tolerance rather than bitwise)."""
+    from picotron_amd.model import build_llama
+    cfg = _cfg(golden_loss)
+    toks = torch.randint(0, cfg.vocab_size, (2, 129), device="cuda", generator=torch.Generator("cuda").manual_seed(3))
+    outs = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("PICO_UNFUSED", mode)
+        torch.manual_seed(7)
+        m = build_llama(cfg, "cuda", BF)
+        with torch.no_grad():  # non-zero LM head so every parameter gets a gradient
+            m.final_proj.weight.normal_(0, 0.02, generator=torch.Generator("cuda").manual_seed(1))
+        logits = m(toks[:, :-1])
+        loss = torch.nn.functional.cross_entropy(logits.reshape(-1, cfg.vocab_size).float(), toks[:, 1:].reshape(-1))
+        loss.backward()
+        outs[mode] = (logits.detach().float(), {n: p.grad.float() for n, p in m.named_parameters()})
+    from conftest import rel_l2
+    assert rel_l2(outs["0"][0].cpu(), outs["1"][0].cpu()) < 1e-2
+    for n in outs["0"][1]:
+        assert rel_l2(outs["0"][1][n].cpu(), outs["1"][1][n].cpu()) < 3e-2, n
