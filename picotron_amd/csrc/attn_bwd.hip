@@ -6,15 +6,22 @@
 // which recomputes P from the (global) O and LSE:  P = exp(scale*QK^T - LSE), dV = P^T dO,
 // dP = dO V^T, delta = rowsum(dO * O), dS = P * (dP - delta), dQ = scale * dS K, dK = scale * dS^T Q.
 //
-// Structure: one workgroup = 8 waves = 256 keys of one (batch, kv-head); wave w owns keys
-// 32w..32w+31 with the key on the MFMA lane, keeps dK^T/dV^T of its keys in accumulators for the
+// attn_bwd_pre_kernel: delta and LSE*log2(e) into [B*Hq][Sq_pad] fp32 arrays (padding rows get
+// LSE = +inf, delta = 0, so padded query rows contribute P = dS = 0 without any masking).
+// attn_bwd_kernel: one workgroup = 8 waves = 256 keys of one (batch, kv-head); wave w owns keys
+// 32w..32w+31 with the key on the MFMA lane and keeps dK^T/dV^T of its keys in accumulators for the
 // whole sweep over (q-heads of the group) x (32-row query tiles), so dK/dV need no cross-workgroup
-// sum. S and dP are computed with the key on the lane, which makes their accumulators directly the
-// A operand of dV = P^T dO and dK = dS^T Q (the dO / Q tile is read transposed with
-// ds_read_b64_tr_b16). dS crosses LDS once for dQ = dS K, computed as 16x16 tiles over all 256 keys
-// over all 256 keys, and each workgroup writes its fp32 dQ partial with plain stores into its key
-// block's slab; attn_bwd_dq_kernel sums the slabs in key-block order (no atomics: plain stores run
-// ~4-5x the chip's float-atomic rate, and the result is bitwise reproducible).
+// sum. Per tile:
+//   * Q, dO (XOR-swizzled row-major images serving both row and transposed reads) and the tile's
+//     LSE/delta arrive by LDS-DMA (global_load_lds_dwordx4) into a 3-slot ring, two tiles ahead, so
+//     HBM/L2 latency hides under two tiles of compute; one barrier opens each tile;
+//   * S, dP (MFMA, key on the lane) -> P, dS (VALU) -> dV += P^T dO, dK += dS^T Q (MFMA; the dO / Q
+//     operand read transposed with ds_read_b64_tr_b16);
+//   * dS crosses LDS once as a [key][q] image written with 4 ds_write_b64 per lane, then
+//     dQ partial = dS K over the block's keys (16x16x32 MFMAs, both operands by transposed reads)
+//     is stored in fp32 to this key block's slab; attn_bwd_dq_kernel sums the slabs in key-block
+//     order (no atomics: plain stores run ~4-5x the chip's float-atomic rate, and the result is
+//     bitwise reproducible).
 // FLOPs per (b, h): 10 * Sq * Sk * D (halved by the causal mask); 2.5x the forward.
 #include "attn_common.h"
 
@@ -22,35 +29,60 @@ namespace {
 
 constexpr int BK = 256;  // keys per workgroup
 constexpr int BQ = 32;   // query rows per tile
+constexpr int NBUF = 3;  // ring slots (prefetch distance 2)
 
 template <int D>
-struct BwdSmem {
-  char k[BK * D * 2];        // K image [key][d] (B operand of S, transposed B operand of dQ)
-  char q[2][BQ * D * 2];     // Q tiles [q][d], double-buffered
-  char dout[2][BQ * D * 2];  // dO tiles [q][d], double-buffered
-  char ds[BQ * BK * 2];      // dS image [q][key], chunk-swizzled
-  float lse2[2][BQ];         // LSE * log2(e)
-  float delta[2][BQ];
+struct BwdCfg {
+  static constexpr int KS = D / 16, DT = D / 32, CPR = D / 8;
+  static constexpr int RB = D * 2;              // bytes per Q/dO/K image row
+  static constexpr int QIMG = BQ * RB;          // one Q (or dO) tile image
+  static constexpr int LSD = 1024;              // LSE*log2e [32] | delta [32] (one DMA piece)
+  static constexpr int SLOT = 2 * QIMG + LSD;
+  static constexpr int KIMG = BK * RB;
+  static constexpr int DSIMG = BK * BQ * 2;     // dS^T [key][q] bf16, 64-B rows
+  static constexpr int SMEM = KIMG + NBUF * SLOT + DSIMG;
+  static constexpr int RPP = 1024 / RB;         // image rows per 1-KiB DMA piece
+  static constexpr int NQP = QIMG / 1024;       // pieces per Q (or dO) tile
+  static constexpr int NP = 2 * NQP + 1;        // pieces per tile
+  static constexpr int NPW = (NP + 7) / 8;      // max pieces per wave
 };
 
-PICO_DEV int ds_off(int q, int key) {
-  // 512-B rows of 32 chunks; low 4 chunk bits XOR (q & 15)
-  const int chunk = key >> 3;
-  return q * 512 + 16 * (chunk ^ (q & 15)) + (key & 7) * 2;
+// XOR applied to the 16-B chunk index of image row `row` (see lds_off in attn_common.h)
+template <int D>
+PICO_DEV int swz(int row) {
+  if constexpr (D == 128) return ((row & 3) << 2) | ((row >> 2) & 3);
+  const int y = (row >> 1) & 7;
+  return y ^ ((y & 1) << 2);
 }
 
-// delta[b, h, q] = sum_d dO * O  (fp32)
+// byte offset of q-pair column `q` (even) of key row `key` in the dS^T image: 64-B rows, the two
+// 32-B halves swapped on odd 8-row groups (conflict-free transposed reads over 8-row strides)
+PICO_DEV int ds_img_off(int key, int q) {
+  return key * 64 + ((((q >> 4) ^ (key >> 3)) & 1) << 5) + ((q & 15) << 1);
+}
+
+// delta[bh, q] = sum_d dO * O, lse2[bh, q] = LSE * log2(e); rows q in [Sq, Sq_pad) get delta = 0 and
+// lse2 = +inf. Rows are ordered (b, h, q) so the LSE reads and the delta / lse2 writes are contiguous;
+// each row of O / dO is one contiguous 2D-byte segment read by D/8 lanes.
 template <int D>
-__global__ __launch_bounds__(256) void attn_bwd_pre_kernel(const pico_attn_args a, float* __restrict__ delta) {
+__global__ __launch_bounds__(256) void attn_bwd_pre_kernel(const pico_attn_args a, float* __restrict__ delta,
+                                                           float* __restrict__ lse2, int sq_pad) {
   constexpr int LPR = D / 8;  // lanes per row (8 bf16 each)
-  const int64_t rows = a.batch * a.seqlen_q * a.heads_q;
+  const int64_t rows = a.batch * a.heads_q * (int64_t)sq_pad;
   const int64_t row = ((int64_t)blockIdx.x * 256 + threadIdx.x) / LPR;
   const int sub = threadIdx.x % LPR;
   if (row >= rows) return;
-  const int hq = (int)(row % a.heads_q);
-  const int64_t bq = row / a.heads_q;
-  const int q = (int)(bq % a.seqlen_q);
-  const int b = (int)(bq / a.seqlen_q);
+  const int q = (int)(row % sq_pad);
+  const int64_t bh = row / sq_pad;
+  const int hq = (int)(bh % a.heads_q);
+  const int b = (int)(bh / a.heads_q);
+  if (q >= a.seqlen_q) {
+    if (sub == 0) {
+      delta[row] = 0.f;
+      lse2[row] = INFINITY;
+    }
+    return;
+  }
   const u16x8 ov = *reinterpret_cast<const u16x8*>((const bf16_t*)a.o + b * a.o_strides[0] + q * a.o_strides[1] +
                                                    hq * a.o_strides[2] + sub * 8);
   const u16x8 dv = *reinterpret_cast<const u16x8*>((const bf16_t*)a.dout + b * a.do_strides[0] +
@@ -60,25 +92,25 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(const pico_attn_args 
   for (int j = 0; j < 8; ++j) s += bf2f(ov[j]) * bf2f(dv[j]);
 #pragma unroll
   for (int o = LPR / 2; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
-  if (sub == 0) delta[((int64_t)b * a.heads_q + hq) * a.seqlen_q + q] = s;
+  if (sub == 0) {
+    delta[row] = s;
+    lse2[row] = a.lse[bh * a.seqlen_q + q] * LOG2E;
+  }
 }
 
-// Main backward kernel. Per tile (32 query rows of one q-head):
-//   load-ahead: the NEXT tile's Q/dO/LSE/delta go global -> registers before this tile's MFMAs and
-//   registers -> the other LDS buffer after them (T14), so HBM latency hides under compute;
-//   S, dP (MFMA) -> P, dS (VALU) -> dV += P^T dO, dK += dS^T Q (MFMA) -> dS to LDS -> barrier ->
-//   dQ partial = dS K over the workgroup's 256 keys (16x16 tiles, one per wave) -> plain fp32 stores
-//   into this key block's slab (summed by attn_bwd_dq_kernel in a fixed order: no atomics,
-//   bitwise reproducible) -> barrier.
+template <int D>
+constexpr int bwd_waves_per_eu() { return D == 64 ? 2 : 1; }
+
 template <int D, bool CAUSAL>
-__global__ __launch_bounds__(512, 2) void attn_bwd_kernel(const pico_attn_args a, float scale, float scale_log2,
-                                                          const float* __restrict__ delta_g, float* __restrict__ dq_part,
-                                                          int64_t slab) {
-  constexpr int CPR = D / 8;
-  constexpr int KS = D / 16;
-  constexpr int DT = D / 32;
-  constexpr int NCH = 2 * BQ * CPR / 512;  // staged 16-B chunks per thread (Q and dO)
-  __shared__ __attribute__((aligned(16))) BwdSmem<D> sm;
+__global__ __launch_bounds__(512, bwd_waves_per_eu<D>()) void attn_bwd_kernel(
+    const pico_attn_args a, float scale, float scale_log2, const float* __restrict__ delta_g,
+    const float* __restrict__ lse2_g, int sq_pad, float* __restrict__ dq_part, int64_t slab) {
+  using C = BwdCfg<D>;
+  constexpr int KS = C::KS, DT = C::DT, CPR = C::CPR;
+  __shared__ __attribute__((aligned(16))) char smem[C::SMEM];
+  char* kimg = smem;
+  char* ring = smem + C::KIMG;
+  char* dsimg0 = smem + C::KIMG + NBUF * C::SLOT;  // dS^T [key][q] of the current tile
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (scalar branches)
@@ -101,12 +133,66 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_kernel(const pico_attn_args a
   const bf16_t* kg = (const bf16_t*)a.k + b * a.k_strides[0] + hk * a.k_strides[2];
   const bf16_t* vg = (const bf16_t*)a.v + b * a.v_strides[0] + hk * a.v_strides[2];
 
+  const int qstart = CAUSAL ? k0 : 0;  // k0 is a multiple of BQ
+  const int nqt = Sq > qstart ? (Sq - qstart + BQ - 1) / BQ : 0;
+  const int ntiles = G * nqt;
+
+  // ---- tile DMA: piece j is issued by wave j % 8 ----
+  //  j < NQP: Q rows RPP*j + lane / CPR, LDS chunk lane % CPR  <- source chunk (lane % CPR) ^ swz(row)
+  //  j < 2 NQP: the same for dO;  j == 2 NQP: lanes 0-7 LSE*log2e[q0 .. q0+31], 8-15 delta (16..63 repeat)
+  const int my_np = (C::NP / 8) + (wave < C::NP % 8 ? 1 : 0);  // wave-uniform piece count
+  int pc_row[C::NPW], pc_col[C::NPW], pc_kind[C::NPW];
+  unsigned pc_dst[C::NPW];
+#pragma unroll
+  for (int i = 0; i < C::NPW; ++i) {
+    const int j = wave + 8 * i;
+    if (j < 2 * C::NQP) {
+      const int jj = j % C::NQP, row = C::RPP * jj + lane / CPR;
+      pc_kind[i] = j < C::NQP ? 0 : 1;
+      pc_row[i] = row;
+      pc_col[i] = 8 * ((lane % CPR) ^ swz<D>(row));
+      pc_dst[i] = (j < C::NQP ? 0 : C::QIMG) + jj * 1024;
+    } else {
+      const int l = lane & 15;
+      pc_kind[i] = 2;
+      pc_row[i] = 4 * (l & 7);
+      pc_col[i] = l >> 3;  // 0: LSE, 1: delta
+      pc_dst[i] = 2 * C::QIMG;
+    }
+  }
+  auto issue = [&](int t) __attribute__((always_inline)) {
+    const int hq = hk * G + t / nqt;
+    const int q0 = qstart + (t % nqt) * BQ;
+    char* slot = ring + (unsigned)(t % NBUF) * (unsigned)C::SLOT;
+    const bool full = q0 + BQ <= Sq;
+#pragma unroll
+    for (int i = 0; i < C::NPW; ++i) {
+      if (i < my_np) {
+        const void* src;
+        if (pc_kind[i] == 2) {
+          const float* base = pc_col[i] ? delta_g : lse2_g;
+          src = base + ((int64_t)b * Hq + hq) * sq_pad + q0 + pc_row[i];
+        } else {
+          const int q = full ? q0 + pc_row[i] : min(q0 + pc_row[i], Sq - 1);
+          src = pc_kind[i] == 0
+                    ? (const bf16_t*)a.q + b * a.q_strides[0] + hq * a.q_strides[2] + (int64_t)q * a.q_strides[1] + pc_col[i]
+                    : (const bf16_t*)a.dout + b * a.do_strides[0] + hq * a.do_strides[2] + (int64_t)q * a.do_strides[1] +
+                          pc_col[i];
+        }
+        __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(slot + pc_dst[i]), 16, 0, 0);
+      }
+    }
+  };
+  // first two tiles go out before the K/V prologue loads
+  if (ntiles > 0) issue(0);
+  if (ntiles > 1) issue(1);
+
   // ---- K block -> LDS image; V fragments -> registers (B operand of dP = dO V^T) ----
   for (int id = threadIdx.x; id < BK * CPR; id += 512) {
     const int row = id / CPR, ch = id % CPR;
     const int key = k0 + row;
     const u16x8 v = *reinterpret_cast<const u16x8*>(kg + (int64_t)min(key, Sk - 1) * a.k_strides[1] + ch * 8);
-    *reinterpret_cast<u16x8*>(sm.k + lds_off<D>(row, ch)) = key < Sk ? v : (u16x8)0;
+    *reinterpret_cast<u16x8*>(kimg + lds_off<D>(row, ch)) = key < Sk ? v : (u16x8)0;
   }
   bf16x8 vf[KS];
   {
@@ -126,94 +212,98 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_kernel(const pico_attn_args a
     dv[dt] = (f32x16)0.f;
   }
 
-  const int qstart = CAUSAL ? k0 : 0;  // k0 is a multiple of BQ
-  const int nqt = Sq > qstart ? (Sq - qstart + BQ - 1) / BQ : 0;
-  const int ntiles = G * nqt;
-
-  // ---- tile staging (global -> registers -> LDS) ----
-  // Thread roles are fixed for the whole sweep: chunk j of this thread stages Q (which == 0) or dO
-  // rows; the role is wave-uniform (D = 64: waves 0-3 vs 4-7; D = 128: by j), so base pointers and
-  // strides are selected once, in scalar registers. Loads read a clamped row unconditionally; the
-  // zero-fill of padded rows is applied at the LDS write so nothing waits right after a load.
-  const bf16_t* stg_base[NCH];
-  int64_t stg_hs[NCH], stg_ss[NCH];
-#pragma unroll
-  for (int j = 0; j < NCH; ++j) {
-    const int which = __builtin_amdgcn_readfirstlane((int)((threadIdx.x + 512 * j) / (BQ * CPR)));
-    stg_base[j] = which == 0 ? (const bf16_t*)a.q + b * a.q_strides[0] : (const bf16_t*)a.dout + b * a.do_strides[0];
-    stg_hs[j] = which == 0 ? a.q_strides[2] : a.do_strides[2];
-    stg_ss[j] = which == 0 ? a.q_strides[1] : a.do_strides[1];
-  }
-  const float* stg_cbase = threadIdx.x < BQ ? a.lse : delta_g;
-  u16x8 stg[NCH];
-  float stg_c = 0.f;
-  auto gload = [&](int t) {
+  // dQ partial [q][d] = scale * dS[q][:] K[:][d] over this block's keys for tile t (16x16 tiles, one
+  // (or two, D=128) per wave; both operands by transposed reads), stored fp32 into the key block's slab.
+  auto dq_tile = [&](int t) __attribute__((always_inline)) {
     const int hq = hk * G + t / nqt;
     const int q0 = qstart + (t % nqt) * BQ;
+    const char* dsimg = dsimg0;
+    constexpr int NT = (BQ / 16) * (D / 16);
+    int kmax = min(BK, Sk - k0);
+    if (CAUSAL) kmax = min(kmax, q0 + BQ - k0);
+    const int g16 = lane >> 4, i16 = lane & 15;
 #pragma unroll
-    for (int j = 0; j < NCH; ++j) {
-      const int rem = (threadIdx.x + 512 * j) % (BQ * CPR);
-      const int row = rem / CPR, ch = rem % CPR;
-      const int qc = min(q0 + row, Sq - 1);
-      stg[j] = *reinterpret_cast<const u16x8*>(stg_base[j] + hq * stg_hs[j] + (int64_t)qc * stg_ss[j] + ch * 8);
-    }
-    const int qc = min(q0 + (int)(threadIdx.x & (BQ - 1)), Sq - 1);
-    stg_c = stg_cbase[((int64_t)b * Hq + hq) * Sq + qc];
-  };
-  auto swrite = [&](int buf, int t) {
-    const int q0 = qstart + (t % nqt) * BQ;
+    for (int tt = 0; tt < NT / 8; ++tt) {
+      const int tl = wave + 8 * tt;
+      const int qi = tl / (D / 16), di = tl % (D / 16);
+      f32x4 acc = (f32x4)0.f;
+      for (int kk = 0; kk < kmax; kk += 32) {
+        {
+          // A = dS[q = 16 qi + (lane & 15)][key = kk + 8 g16 + j]: transposed read of the [key][q] image
+          const int row = kk + 8 * g16 + (i16 >> 2);
+          const int qc = 16 * qi + 4 * (i16 & 3);
+          const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(dsimg + ds_img_off(row, qc)));
+          const i16x4 up = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(dsimg + ds_img_off(row + 4, qc)));
+          typedef __attribute__((ext_vector_type(8))) short i16x8;
+          const i16x8 av = {lo[0], lo[1], lo[2], lo[3], up[0], up[1], up[2], up[3]};
+          const bf16x8 bf = lds_read_tr16<D>(kimg, kk, di * 16, lane);
+          acc = mfma16(__builtin_bit_cast(bf16x8, av), bf, acc);
+        }
+      }
+      float* dst = dq_part + kb * slab + (int64_t)b * Sq * Hq * D + hq * D + di * 16 + i16;
 #pragma unroll
-    for (int j = 0; j < NCH; ++j) {
-      const int c = threadIdx.x + 512 * j;
-      const int which = c / (BQ * CPR), rem = c % (BQ * CPR);
-      const int row = rem / CPR, ch = rem % CPR;
-      char* dst = which == 0 ? sm.q[buf] : sm.dout[buf];
-      *reinterpret_cast<u16x8*>(dst + lds_off<D>(row, ch)) = q0 + row < Sq ? stg[j] : (u16x8)0;
+      for (int j = 0; j < 4; ++j) {
+        const int q = q0 + qi * 16 + 4 * g16 + j;
+        if (q < Sq) dst[(int64_t)q * Hq * D] = acc[j] * scale;
+      }
     }
-    const bool ok = q0 + (int)(threadIdx.x & (BQ - 1)) < Sq;
-    if (threadIdx.x < BQ)
-      sm.lse2[buf][threadIdx.x] = ok ? stg_c * LOG2E : INFINITY;  // +inf LSE -> P = 0 for padded rows
-    else if (threadIdx.x < 2 * BQ)
-      sm.delta[buf][threadIdx.x - BQ] = ok ? stg_c : 0.f;
   };
-
-  if (ntiles > 0) {
-    gload(0);
-    swrite(0, 0);
-  }
-  __syncthreads();
 
   for (int t = 0; t < ntiles; ++t) {
-    const int buf = t & 1;
+    // this wave's pieces of tile t landed (tile t+1's stay in flight), then everyone's (barrier);
+    // the barrier also retires every read of iteration t-1 (ring slot (t+2) % 3, dS image)
+    if (t + 1 < ntiles) {
+      if (my_np == C::NPW) {
+        if constexpr (C::NPW == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+      } else {
+        if constexpr (C::NPW == 2) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      }
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    if (t + 2 < ntiles) issue(t + 2);
+
     const int hq = hk * G + t / nqt;
     const int q0 = qstart + (t % nqt) * BQ;
-    const bool more = t + 1 < ntiles;
-    if (more) gload(t + 1);
+    const char* slot = ring + (unsigned)(t % NBUF) * (unsigned)C::SLOT;
+    const char* qs = slot;
+    const char* dos = slot + C::QIMG;
+    const float* lsd = (const float*)(slot + 2 * C::QIMG);
 
     const bool active = !CAUSAL || kw <= q0 + BQ - 1;
     if (active) {
-      const char* qs = sm.q[buf];
-      const char* dos = sm.dout[buf];
       // S[q][key] and dP[q][key]: A = Q / dO rows (LDS), B = K^T (LDS) / V^T (registers)
       f32x16 s = (f32x16)0.f, dp = (f32x16)0.f;
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
         const bf16x8 qa = lds_read_b128(qs, lds_off<D>(r, 2 * ks + h));
-        const bf16x8 kbf = lds_read_b128(sm.k, lds_off<D>(32 * wave + r, 2 * ks + h));
+        const bf16x8 kbf = lds_read_b128(kimg, lds_off<D>(32 * wave + r, 2 * ks + h));
         s = mfma32(qa, kbf, s);
         const bf16x8 da = lds_read_b128(dos, lds_off<D>(r, 2 * ks + h));
         dp = mfma32(da, vf[ks], dp);
       }
-      // P = exp2(S * scale*log2e - LSE*log2e) (in s), dS = P * (dP - delta) (in dp); lane: key my_key
-      const bool need_mask = (CAUSAL && kw + 31 > q0) || (k0 + BK > Sk);
+      // rows of this lane's accumulator registers: q = 8g + 4h + (0..3), g = 0..3
+      f32x4 l2[4], dl[4];
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int qi = acc_row(i, h);
-        float pv = fast_exp2(s[i] * scale_log2 - sm.lse2[buf][qi]);
-        if (need_mask) pv = ((CAUSAL && my_key > q0 + qi) || my_key >= Sk) ? 0.f : pv;
-        s[i] = pv;
-        dp[i] = pv * (dp[i] - sm.delta[buf][qi]);
+      for (int g = 0; g < 4; ++g) {
+        l2[g] = *reinterpret_cast<const f32x4*>(lsd + 8 * g + 4 * h);
+        dl[g] = *reinterpret_cast<const f32x4*>(lsd + 32 + 8 * g + 4 * h);
       }
+      // P = exp2(S * scale*log2e - LSE*log2e) (in s), dS = P * (dP - delta) (in dp); lane: key my_key
+#pragma unroll
+      for (int i = 0; i < 16; ++i) s[i] = fast_exp2(__builtin_fmaf(s[i], scale_log2, -l2[i >> 2][i & 3]));
+      if ((CAUSAL && kw + 31 > q0) || (k0 + BK > Sk)) {  // wave-uniform
+        // causal: key > q  <=>  (i&3) + 8(i>>2) < rel;  padding keys: key >= Sk
+        const int rel = CAUSAL ? my_key - q0 - 4 * h : -1;
+        const bool kill_all = my_key >= Sk;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) s[i] = ((i & 3) + 8 * (i >> 2) < rel || kill_all) ? 0.f : s[i];
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) dp[i] = s[i] * (dp[i] - dl[i >> 2][i & 3]);
       // dV[key][d] += P^T dO ; dK[key][d] += dS^T Q   (k index = query rows of the tile)
 #pragma unroll
       for (int st = 0; st < 2; ++st) {
@@ -233,39 +323,19 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_kernel(const pico_attn_args a
           dk[dt] = mfma32(sf, qf, dk[dt]);
         }
       }
-      // dS (bf16) -> LDS image [q][key] for dQ
+      // dS^T image [key][q] (bf16): registers 4g..4g+3 are q = 8g + 4h + 0..3 -> one 8-B store each
+      char* dsimg = dsimg0;
+      const int krow = 32 * wave + r;
 #pragma unroll
-      for (int i = 0; i < 16; ++i)
-        *reinterpret_cast<bf16_t*>(sm.ds + ds_off(acc_row(i, h), 32 * wave + r)) = f2bf(dp[i]);
-    }
-    __syncthreads();  // dS visible
-
-    // ---- dQ partial [q][d] = scale * dS[q][:] K[:][d] over this block's keys: 16x16 tiles ----
-    {
-      constexpr int NT = (BQ / 16) * (D / 16);
-      int kmax = min(BK, Sk - k0);
-      if (CAUSAL) kmax = min(kmax, ((q0 + BQ - 1 - k0) / 32 + 1) * 32);
-      kmax = (kmax + 31) & ~31;
+      for (int g = 0; g < 4; ++g) {
+        u16x4 w;
 #pragma unroll
-      for (int tt = 0; tt < NT / 8; ++tt) {
-        const int tl = wave + 8 * tt;
-        const int qi = tl / (D / 16), di = tl % (D / 16);
-        f32x4 acc = (f32x4)0.f;
-        for (int kk = 0; kk < kmax; kk += 32) {
-          const bf16x8 af = lds_read_b128(sm.ds, ds_off(qi * 16 + (lane & 15), kk + 8 * (lane >> 4)));
-          const bf16x8 bf = lds_read_tr16<D>(sm.k, kk, di * 16, lane);
-          acc = mfma16(af, bf, acc);
-        }
-        float* dst = dq_part + kb * slab + (int64_t)b * Sq * Hq * D + hq * D + di * 16 + (lane & 15);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int q = q0 + qi * 16 + 4 * (lane >> 4) + j;
-          if (q < Sq) dst[(int64_t)q * Hq * D] = acc[j] * scale;
-        }
+        for (int j = 0; j < 4; ++j) w[j] = f2bf(dp[4 * g + j]);
+        *reinterpret_cast<u16x4*>(dsimg + ds_img_off(krow, 8 * g + 4 * h)) = w;
       }
     }
-    if (more) swrite(buf ^ 1, t + 1);
-    __syncthreads();  // next tile staged; dS reads done
+    __syncthreads();  // dS visible
+    dq_tile(t);
   }
 
   // ---- epilogue: dK = scale * acc, dV = acc; lane holds d = 32 dt + r, keys kw + acc_row(i, h) ----
@@ -324,30 +394,39 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const pico_attn_args a
                             sub * 8) = o;
 }
 
-int64_t delta_floats(const pico_attn_args* a) {
-  const int64_t nrow = a->batch * a->heads_q * a->seqlen_q;
-  return ((nrow + 63) / 64) * 64;
+int sq_padded(const pico_attn_args* a) { return (int)((a->seqlen_q + BQ - 1) / BQ) * BQ; }
+
+// [lse2 | delta], each [B*Hq][Sq_pad] fp32, rounded up to 64 floats
+int64_t lsd_floats(const pico_attn_args* a) {
+  const int64_t n = a->batch * a->heads_q * (int64_t)sq_padded(a);
+  return ((n + 63) / 64) * 64;
 }
 
 template <int D>
 int launch_bwd(const pico_attn_args* a, hipStream_t s) {
   const int f32acc = (a->flags & PICO_ATTN_DQ_F32_ACCUM) != 0;
-  float* delta = (float*)a->workspace;
-  float* dq_part = delta + delta_floats(a);
+  const int sq_pad = sq_padded(a);
+  float* lse2 = (float*)a->workspace;
+  float* delta = lse2 + lsd_floats(a);
+  float* dq_part = delta + lsd_floats(a);
   const int64_t slab = a->batch * a->seqlen_q * a->heads_q * D;
   const int64_t rows = a->batch * a->seqlen_q * a->heads_q;
   const int row_blocks = pico_cdiv(rows * (D / 8), 256);
-  PICO_LAUNCH(PICO_K_ATTN_BWD_PRE, "attn_bwd_pre", s, attn_bwd_pre_kernel<D><<<row_blocks, 256, 0, s>>>(*a, delta));
+  const int pre_blocks = pico_cdiv(a->batch * a->heads_q * (int64_t)sq_pad * (D / 8), 256);
+  PICO_LAUNCH(PICO_K_ATTN_BWD_PRE, "attn_bwd_pre", s,
+              attn_bwd_pre_kernel<D><<<pre_blocks, 256, 0, s>>>(*a, delta, lse2, sq_pad));
   const int nkb = (int)((a->seqlen_k + BK - 1) / BK);
   const int64_t nblk = (int64_t)nkb * a->batch * a->heads_kv;
   const float sl2 = a->softmax_scale * LOG2E;
   if (nblk > 0) {
     if (a->causal) {
       PICO_LAUNCH(PICO_K_ATTN_BWD, "attn_bwd", s,
-                  attn_bwd_kernel<D, true><<<(int)nblk, 512, 0, s>>>(*a, a->softmax_scale, sl2, delta, dq_part, slab));
+                  attn_bwd_kernel<D, true><<<(int)nblk, 512, 0, s>>>(*a, a->softmax_scale, sl2, delta, lse2, sq_pad,
+                                                                     dq_part, slab));
     } else {
       PICO_LAUNCH(PICO_K_ATTN_BWD, "attn_bwd", s,
-                  attn_bwd_kernel<D, false><<<(int)nblk, 512, 0, s>>>(*a, a->softmax_scale, sl2, delta, dq_part, slab));
+                  attn_bwd_kernel<D, false><<<(int)nblk, 512, 0, s>>>(*a, a->softmax_scale, sl2, delta, lse2, sq_pad,
+                                                                      dq_part, slab));
     }
   }
   if (a->causal) {
@@ -387,9 +466,9 @@ extern "C" {
 int64_t pico_attn_args_size(void) { return (int64_t)sizeof(pico_attn_args); }
 
 int64_t pico_attn_bwd_workspace_bytes(const pico_attn_args* a) {
-  // delta [B*Hq*Sq] fp32 + one fp32 dQ partial slab [B, Sq, Hq, D] per 256-key block
+  // lse2, delta [B*Hq*Sq_pad] fp32 + one fp32 dQ partial slab [B, Sq, Hq, D] per 256-key block
   const int64_t nkb = (a->seqlen_k + BK - 1) / BK;
-  return (delta_floats(a) + nkb * a->batch * a->seqlen_q * a->heads_q * a->head_dim) * 4;
+  return (2 * lsd_floats(a) + nkb * a->batch * a->seqlen_q * a->heads_q * a->head_dim) * 4;
 }
 
 int pico_attn_bwd(const pico_attn_args* a, void* stream) {

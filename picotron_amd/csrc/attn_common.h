@@ -80,6 +80,47 @@ PICO_DEV bf16x8 lds_read_tr16(const char* base, int row0, int col0, int lane) {
   return __builtin_bit_cast(bf16x8, v);
 }
 
+// Transposed 32x32x16 operand from a per-lane address (the caller's layout supplies, for lane
+// (g = lane>>4, q = (lane&15)>>2, p = lane&3), the byte address of row 4*(lane>>5) + q, columns
+// 16*(g&1) + 4p .. +3 of the block): two ds_read_b64_tr_b16, the second `hi` bytes further (8 rows).
+// Result element j of lane (r, h) = T[8*(j>>2) + 4h + (j&3)][r]  (see lds_read_tr32).
+PICO_DEV bf16x8 lds_read_tr_rows(const char* p, int hi) {
+  const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)p);
+  const i16x4 up = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(p + hi));
+  typedef __attribute__((ext_vector_type(8))) short i16x8;
+  i16x8 v = {lo[0], lo[1], lo[2], lo[3], up[0], up[1], up[2], up[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// ds_read_b64_tr_b16 at an LDS byte address + immediate (inline asm: hipcc re-bases DS address
+// chains onto negative offsets it cannot fold, costing a VALU add per read). The compiler does not
+// track these reads: consume them only after lds_wait_all().
+template <int OFF>
+PICO_DEV i16x4 ds_tr16_imm(unsigned addr) {
+  static_assert(OFF >= 0 && OFF < 65536, "DS offset is 16-bit unsigned");
+  i16x4 r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "n"(OFF));
+  return r;
+}
+// Two of them = one 32x32x16 operand (rows +0..3 at OFF, +8..11 at OFF + HI), see lds_read_tr_rows.
+template <int OFF, int HI>
+PICO_DEV bf16x8 tr_operand_imm(unsigned addr) {
+  const i16x4 lo = ds_tr16_imm<OFF>(addr);
+  const i16x4 up = ds_tr16_imm<OFF + HI>(addr);
+  typedef __attribute__((ext_vector_type(8))) short i16x8;
+  i16x8 v = {lo[0], lo[1], lo[2], lo[3], up[0], up[1], up[2], up[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+// Wait for every outstanding LDS read (incl. the inline-asm ones) and stop the scheduler from
+// hoisting their consumers above the wait (cdna_hip_programming.md §5.4 rule 18).
+PICO_DEV void lds_wait_all() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+PICO_DEV unsigned lds_addr(const void* p) {
+  return (unsigned)(uintptr_t)(__attribute__((address_space(3))) const char*)p;
+}
+
 // 8 fp32 accumulator registers -> bf16x8 MFMA operand fragment (round to nearest even).
 PICO_DEV bf16x8 pack_frag(const float* v) {
   bf16x8 r;

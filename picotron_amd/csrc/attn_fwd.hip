@@ -10,12 +10,20 @@
 //   * K and V tiles are register-staged into a double-buffered, XOR-swizzled LDS image: the next
 //     tile's global loads are issued before this tile's MFMAs and written to LDS after them (T14).
 //   * Swapped product S^T = K * Q^T (v_mfma_f32_32x32x16_bf16): the accumulator has the query on
-//     the lane and 16 keys in registers, so the online softmax is lane-local (one xor-32 shuffle
+//     the lane and 16 keys in registers, so the online softmax is lane-local (one permlane32 swap
 //     for the row max) and P^T is already the B operand of O^T += V^T * P^T (no LDS round trip);
 //     V^T fragments come from ds_read_b64_tr_b16 on the row-major V image.
+//   * The softmax is written for the VALU budget, which (not the MFMA) bounds D = 64: raw scores
+//     are kept unscaled and one FMA per score folds scale*log2(e) and the running max into the
+//     exp2 argument; the row sum stays a per-lane partial until the epilogue; O is rescaled only
+//     when some row's max grew (wave-uniform vote; exact, no threshold); masking (causal diagonal,
+//     key padding) is a separate branch-free body used only on the tiles that need it.
 //   * Causal: tiles beyond the diagonal are never loaded; waves skip tiles entirely above their rows;
-//     workgroups are issued heaviest-first over all heads (LPT order).
+//     workgroups are issued heaviest-first over all heads (LPT order), and the q-blocks of one head
+//     sit nbh (a multiple of 8) block ids apart, i.e. on one XCD, sharing its L2 for K/V.
 // FLOPs per (b, h): 4 * Sq * Sk * D (halved by the causal mask).
+#include <type_traits>
+
 #include "attn_common.h"
 
 namespace {
@@ -23,19 +31,48 @@ namespace {
 constexpr int BM = 128;  // query rows per workgroup (32 per wave)
 constexpr int BN = 64;   // keys per tile
 
+// LDS images (one per buffer), chosen so that every read of a tile is one per-lane base register
+// plus compile-time immediates, and conflict-free:
+//   K: KS images [64 keys][16 d] (32-B rows), 16-B chunk h of row `key` stored at chunk h ^ bit3(key):
+//      a ds_read_b128 lane group (16 rows, one chunk) covers all 64 banks exactly once;
+//   V: D/32 images [64 keys][32 d] (64-B rows), unswizzled: each 32-lane half of a ds_read_b64_tr_b16
+//      reads 4 consecutive rows x 64 B = 256 contiguous bytes.
+// LDS images (one set per ring slot), chosen so that every read of a tile is one per-lane base
+// register plus compile-time immediates, and conflict-free:
+//   K: KS images [64 keys][16 d] (32-B rows), 16-B chunk h of row `key` stored at chunk h ^ bit3(key):
+//      a ds_read_b128 lane group (16 rows, one chunk) covers all 64 banks exactly once;
+//   V: D/32 images [64 keys][32 d] (64-B rows), unswizzled: each 32-lane half of a ds_read_b64_tr_b16
+//      reads 4 consecutive rows x 64 B = 256 contiguous bytes.
+// Tiles arrive by LDS-DMA (global_load_lds_dwordx4: 1 KiB per wave-instruction, lane-linear in LDS),
+// so the swizzle is applied to the per-lane SOURCE address. NBUF-slot ring, prefetch distance NBUF-1.
 template <int D>
-struct FwdSmem {
-  char k[2][BN * D * 2];
-  char v[2][BN * D * 2];
+struct FwdCfg {
+  static constexpr int KS = D / 16, DT = D / 32;
+  static constexpr int KIMG = BN * 32;                  // bytes per 16-wide K image
+  static constexpr int VIMG = BN * 64;                  // bytes per 32-wide V image
+  static constexpr int SLOT = 2 * BN * D * 2;           // K + V of one tile
+  static constexpr int NBUF = D == 64 ? 3 : 2;          // LDS: 48 KiB (D=64) / 64 KiB (D=128) per WG
+  static constexpr int NI = 2 * KS + 4 * DT;            // 1-KiB DMA pieces per tile
+  static constexpr int NIW = NI / 4;                    // ... per wave
+  static constexpr int WAVES_PER_EU = D == 64 ? 3 : 2;
 };
 
+// max over both lane halves (lane r and r + 32 hold the same query row)
+PICO_DEV float halves_max(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+PICO_DEV float halves_sum(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 template <int D, bool CAUSAL>
-__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const pico_attn_args a, float scale_log2) {
-  constexpr int CPR = D / 8;                   // 16-byte chunks per row
-  constexpr int CHUNKS_PER_THREAD = BN * CPR / 256;
-  constexpr int KS = D / 16;                   // k-steps of the S^T product
-  constexpr int DT = D / 32;                   // 32-wide output tiles of O^T
-  __shared__ __attribute__((aligned(16))) FwdSmem<D> sm;
+__global__ __launch_bounds__(256, FwdCfg<D>::WAVES_PER_EU) void attn_fwd_kernel(const pico_attn_args a, float scale_log2) {
+  using C = FwdCfg<D>;
+  constexpr int KS = C::KS;  // k-steps of the S^T product
+  constexpr int DT = C::DT;  // 32-wide output tiles of O^T
+  __shared__ __attribute__((aligned(16))) char smem[C::NBUF * C::SLOT];
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (scalar branches)
@@ -64,134 +101,188 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const pico_attn_args a
   // ---- Q fragments (B operand of S^T = K Q^T): Q[my_q][16 ks + 8 h + j] ----
   bf16x8 qf[KS];
   {
-    const bool ok = my_q < Sq;
     const bf16_t* qp = qg + (int64_t)min(my_q, Sq - 1) * a.q_strides[1] + 8 * h;
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      const u16x8 v = *reinterpret_cast<const u16x8*>(qp + 16 * ks);
-      qf[ks] = __builtin_bit_cast(bf16x8, ok ? v : (u16x8)0);
-    }
+    for (int ks = 0; ks < KS; ++ks) qf[ks] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u16x8*>(qp + 16 * ks));
   }
 
-  // number of key tiles this workgroup visits
+  // tiles this workgroup visits; the last key any of its rows may see is `wg_lim`
   int kend = Sk;
   if (CAUSAL) kend = min(Sk, q0 + BM);
   const int ntiles = (kend + BN - 1) / BN;
+  // the wave's rows see keys <= lim_w (last row); tiles entirely <= first_lim need no mask
+  const int lim_last = CAUSAL ? min(qw + 31, Sk - 1) : Sk - 1;
+  const int lim_first = CAUSAL ? min(qw, Sk - 1) : Sk - 1;
+  const int lim_lane = CAUSAL ? min(my_q, Sk - 1) : Sk - 1;  // this lane's row: keys <= lim_lane
 
-  // ---- register staging of K/V tiles ----
-  // Loads are issued unconditionally from a clamped row; the zero-fill of rows past Sk is applied
-  // when the registers are written to LDS, so no wait is forced right after the loads.
-  u16x8 kreg[CHUNKS_PER_THREAD], vreg[CHUNKS_PER_THREAD];
-  auto gload = [&](int tile) {
+  // ---- LDS-DMA staging: piece j (wave w issues j = w, w + 4, ...) ----
+  // K piece (j < 2 KS): image ks = j / 2, rows 32 (j & 1) + lane / 2, LDS chunk lane & 1, which holds
+  // source chunk h = (lane & 1) ^ bit3(row). V piece: image dt, rows 16 p + lane / 4, 16-B part lane & 3.
+  // Per piece: this lane's source row within the tile and element column; LDS destination offset.
+  // K and V pieces are uniform per (wave, i), so the K/V choice is a scalar select.
+  int src_row[C::NIW], src_col[C::NIW];
+  unsigned dst_off[C::NIW];
+  bool is_k[C::NIW];
 #pragma unroll
-    for (int c = 0; c < CHUNKS_PER_THREAD; ++c) {
-      const int id = threadIdx.x + 256 * c;
-      const int row = id / CPR, ch = id % CPR;
-      const int kc = min(tile * BN + row, Sk - 1);
-      kreg[c] = *reinterpret_cast<const u16x8*>(kg + (int64_t)kc * ksd + ch * 8);
-      vreg[c] = *reinterpret_cast<const u16x8*>(vg + (int64_t)kc * vsd + ch * 8);
+  for (int i = 0; i < C::NIW; ++i) {
+    const int j = wave + 4 * i;
+    if (j < 2 * KS) {
+      const int ks = j >> 1, row = 32 * (j & 1) + (lane >> 1);
+      src_row[i] = row;
+      src_col[i] = 16 * ks + 8 * ((lane & 1) ^ ((row >> 3) & 1));
+      dst_off[i] = ks * C::KIMG + 32 * (j & 1) * 32;
+      is_k[i] = true;
+    } else {
+      const int jv = j - 2 * KS, dt = jv >> 2, row = 16 * (jv & 3) + (lane >> 2);
+      src_row[i] = row;
+      src_col[i] = 32 * dt + 8 * (lane & 3);
+      dst_off[i] = BN * D * 2 + dt * C::VIMG + 16 * (jv & 3) * 64;
+      is_k[i] = false;
+    }
+  }
+  // element offsets within a tile for full tiles (rows never clamped)
+  unsigned src_off[C::NIW];
+#pragma unroll
+  for (int i = 0; i < C::NIW; ++i) src_off[i] = (unsigned)(src_row[i] * (is_k[i] ? ksd : vsd) + src_col[i]);
+  auto issue = [&](int tile) __attribute__((always_inline)) {
+    char* slot = smem + (unsigned)(tile % C::NBUF) * (unsigned)C::SLOT;
+    const int base = tile * BN;
+    if (base + BN <= Sk) {
+#pragma unroll
+      for (int i = 0; i < C::NIW; ++i) {
+        const bf16_t* tb = is_k[i] ? kg + (int64_t)base * ksd : vg + (int64_t)base * vsd;
+        __builtin_amdgcn_global_load_lds((const void*)(tb + src_off[i]),
+                                         (__attribute__((address_space(3))) void*)(slot + dst_off[i]), 16, 0, 0);
+      }
+    } else {  // last, partial tile: clamp rows (finite values; the softmax masks keys >= Sk)
+#pragma unroll
+      for (int i = 0; i < C::NIW; ++i) {
+        const int key = min(base + src_row[i], Sk - 1);
+        const bf16_t* src = is_k[i] ? kg + (int64_t)key * ksd + src_col[i] : vg + (int64_t)key * vsd + src_col[i];
+        __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(slot + dst_off[i]),
+                                         16, 0, 0);
+      }
     }
   };
-  auto swrite = [&](int buf, int tile) {
-#pragma unroll
-    for (int c = 0; c < CHUNKS_PER_THREAD; ++c) {
-      const int id = threadIdx.x + 256 * c;
-      const int row = id / CPR, ch = id % CPR;
-      const bool ok = tile * BN + row < Sk;
-      const int off = lds_off<D>(row, ch);
-      *reinterpret_cast<u16x8*>(sm.k[buf] + off) = ok ? kreg[c] : (u16x8)0;
-      *reinterpret_cast<u16x8*>(sm.v[buf] + off) = ok ? vreg[c] : (u16x8)0;
-    }
-  };
+
+  // per-lane LDS read offsets (everything else is an immediate)
+  const unsigned smem_lds = lds_addr(smem);
+  const unsigned k_lane = r * 32 + 16 * (h ^ ((r >> 3) & 1));
+  const unsigned v_lane = (4 * h + ((lane & 15) >> 2)) * 64 + 32 * ((lane >> 4) & 1) + 8 * (lane & 3);
 
   f32x16 o[DT];
 #pragma unroll
   for (int dt = 0; dt < DT; ++dt) o[dt] = (f32x16)0.f;
-  float m_i = -INFINITY, l_i = 0.f;
+  float m_i = -INFINITY;  // running max of scale*log2e*s (scaled domain)
+  float l_i = 0.f;        // per-lane partial row sum (this lane's keys only)
 
-  if (ntiles > 0) {
-    gload(0);
-    swrite(0, 0);
-  }
-  __syncthreads();
+  // P^T (keys 32 kt .. 32 kt + 31 of the tile) times V: 2 * DT MFMAs.
+  auto pv_half_impl = [&](const f32x16& p, unsigned va, auto kt_tag) __attribute__((always_inline)) {
+    constexpr int KT = decltype(kt_tag)::value;
+    bf16x8 vf[2][DT];
+    static_for<2>([&](auto st_) {
+      constexpr int ST = decltype(st_)::value;
+      static_for<DT>([&](auto dt_) {
+        constexpr int DTI = decltype(dt_)::value;
+        vf[ST][DTI] = tr_operand_imm<BN * D * 2 + DTI * C::VIMG + (32 * KT + 16 * ST) * 64, 8 * 64>(va);
+      });
+    });
+    float pv[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) pv[j] = p[j];
+    const bf16x8 pf0 = pack_frag(pv), pf1 = pack_frag(pv + 8);
+    lds_wait_all();
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) o[dt] = mfma32(vf[0][dt], pf0, o[dt]);
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) o[dt] = mfma32(vf[1][dt], pf1, o[dt]);
+  };
 
-  for (int t = 0; t < ntiles; ++t) {
-    const int buf = t & 1;
-    const bool more = t + 1 < ntiles;
-    if (more) gload(t + 1);
-    const int n0 = t * BN;
-    // whole tile above this wave's rows (causal) -> nothing to do for this wave
-    const bool active = !CAUSAL || n0 <= qw + 31;
-    if (active) {
-      const char* kb = sm.k[buf];
-      const char* vb = sm.v[buf];
-      f32x16 s[2];
+  // One 64-key tile for this wave. MASK: apply key <= lim_lane (causal) and key < Sk.
+  auto tile_body = [&](const char* kb, unsigned vaddr, int n0, bool mask) __attribute__((always_inline)) {
+    f32x16 s[2];
 #pragma unroll
-      for (int kt = 0; kt < 2; ++kt) {
-        s[kt] = (f32x16)0.f;
+    for (int kt = 0; kt < 2; ++kt) {
+      s[kt] = (f32x16)0.f;
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-          const bf16x8 kf = lds_read_b128(kb, lds_off<D>(kt * 32 + r, 2 * ks + h));
-          s[kt] = mfma32(kf, qf[ks], s[kt]);
-        }
-      }
-      // scale + mask; lane holds query my_q and keys n0 + 32 kt + acc_row(i, h)
-      const bool need_mask = (n0 + BN > Sk) || (CAUSAL && n0 + BN - 1 > qw);
-      float mloc = -INFINITY;
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          float x = s[kt][i] * scale_log2;
-          if (need_mask) {
-            const int key = n0 + kt * 32 + acc_row(i, h);
-            x = (key >= Sk || (CAUSAL && key > my_q)) ? -INFINITY : x;
-          }
-          s[kt][i] = x;
-          mloc = fmaxf(mloc, x);
-        }
-      }
-      mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
-      const float m_new = fmaxf(m_i, mloc);
-      const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
-      const float alpha = fast_exp2(m_i - m_use);
-      float lsum = 0.f;
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const float p = fast_exp2(s[kt][i] - m_use);
-          s[kt][i] = p;
-          lsum += p;
-        }
-      }
-      l_i = l_i * alpha + lsum;
-      m_i = m_new;
-#pragma unroll
-      for (int dt = 0; dt < DT; ++dt) o[dt] *= alpha;
-      // O^T[dt] += V^T * P^T : A = V^T via transposed LDS read, B = packed P^T registers
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt) {
-#pragma unroll
-        for (int st = 0; st < 2; ++st) {
-          float pv[8];
-#pragma unroll
-          for (int j = 0; j < 8; ++j) pv[j] = s[kt][8 * st + j];
-          const bf16x8 pf = pack_frag(pv);
-#pragma unroll
-          for (int dt = 0; dt < DT; ++dt) {
-            const bf16x8 vf = lds_read_tr32<D>(vb, kt * 32 + 16 * st, dt * 32, lane);
-            o[dt] = mfma32(vf, pf, o[dt]);
-          }
-        }
+      for (int ks = 0; ks < KS; ++ks) {
+        const bf16x8 kf = lds_read_b128(kb, ks * C::KIMG + kt * 32 * 32);
+        s[kt] = mfma32(kf, qf[ks], s[kt]);
       }
     }
-    if (more) swrite(buf ^ 1, t + 1);
-    __syncthreads();
+    // lane holds row my_q, keys n0 + 32 kt + acc_row(i, h) = n0 + 4h + c(kt, i)
+    if (mask) {  // wave-uniform
+      const int rel = lim_lane - n0 - 4 * h;  // key allowed iff c <= rel
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int c = 32 * kt + (i & 3) + 8 * (i >> 2);
+          s[kt][i] = c <= rel ? s[kt][i] : -INFINITY;
+        }
+    }
+    float mx = s[0][0];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int i = (kt == 0 ? 1 : 0); i < 16; ++i) mx = fmaxf(mx, s[kt][i]);
+    const float m_tile = halves_max(mx) * scale_log2;
+    // rescale only when some row's max grew (wave-uniform); exact
+    if (__builtin_amdgcn_ballot_w64(m_tile > m_i)) {
+      const float m_new = fmaxf(m_i, m_tile);
+      const float alpha = m_i == -INFINITY ? 0.f : fast_exp2(m_i - m_new);
+      l_i *= alpha;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) o[dt] *= alpha;
+      m_i = m_new;
+    }
+    const float neg_m = m_i == -INFINITY ? 0.f : -m_i;
+    float lsum0 = 0.f, lsum1 = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int i = 0; i < 16; i += 2) {
+        const float p0 = fast_exp2(__builtin_fmaf(s[kt][i], scale_log2, neg_m));
+        const float p1 = fast_exp2(__builtin_fmaf(s[kt][i + 1], scale_log2, neg_m));
+        s[kt][i] = p0;
+        s[kt][i + 1] = p1;
+        lsum0 += p0;
+        lsum1 += p1;
+      }
+    l_i += lsum0 + lsum1;
+    // O^T[dt] += V^T * P^T : A = V^T via transposed LDS reads (per kt: 2 st x DT operands, issued
+    // together, one wait), B = packed P^T registers
+    pv_half_impl(s[0], vaddr, std::integral_constant<int, 0>{});
+    pv_half_impl(s[1], vaddr, std::integral_constant<int, 1>{});
+  };
+
+  constexpr int P = C::NBUF - 1;  // prefetch distance
+#pragma unroll
+  for (int t = 0; t < P; ++t)
+    if (t < ntiles) issue(t);
+
+  for (int t = 0; t < ntiles; ++t) {
+    // tile t's pieces landed (this wave's), then every wave's (barrier); later tiles stay in flight
+    if (P == 2 && t + 1 < ntiles) {
+      if constexpr (C::NIW == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    // slot (t + P) % NBUF was last read in iteration t - 1, which every wave has finished
+    if (t + P < ntiles) issue(t + P);
+    const int n0 = t * BN;
+    // wave-uniform: skip (tile above every row), full (every key visible to every row), or masked
+    if (n0 <= lim_last) {
+      const unsigned slot = (unsigned)(t % C::NBUF) * (unsigned)C::SLOT;
+      const char* kb = smem + (slot + k_lane);
+      tile_body(kb, smem_lds + slot + v_lane, n0, n0 + BN - 1 > lim_first);
+    }
   }
 
   // ---- epilogue: O = O^T / l, LSE = (m + log2 l) * ln2 ----
-  const float l_tot = l_i + __shfl_xor(l_i, 32, 64);
+  const float l_tot = halves_sum(l_i);
   if (my_q < Sq) {
     const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
     bf16_t* op = (bf16_t*)a.o + b * a.o_strides[0] + hq * a.o_strides[2] + (int64_t)my_q * a.o_strides[1];
@@ -219,6 +310,7 @@ int launch_fwd(const pico_attn_args* a, hipStream_t s) {
   const int64_t nblk = (int64_t)nmb * a->batch * a->heads_q;
   PICO_REQUIRE(nblk < (1ll << 31), "pico_attn_fwd: grid too large");
   const float sl2 = a->softmax_scale * LOG2E;
+  PICO_REQUIRE(sl2 > 0.f, "pico_attn_fwd: softmax_scale must be positive");
   if (a->causal) {
     PICO_LAUNCH(PICO_K_ATTN_FWD, "attn_fwd", s, attn_fwd_kernel<D, true><<<(int)nblk, 256, 0, s>>>(*a, sl2));
   } else {

@@ -4,6 +4,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include <type_traits>
 #include "../../include/picotron_hip.h"
 
 typedef uint16_t bf16_t;  // raw bf16 bits on the host/kernel ABI
@@ -52,5 +54,14 @@ void pico_prof_post(int kid, hipStream_t s);
     int _rc = pico_check_launch(opname);               \
     if (_rc) return _rc;                               \
   } while (0)
+
+// Compile-time loop: f(std::integral_constant<int, I>{}) for I = 0 .. N-1.
+template <int N, int I = 0, class F>
+__host__ __device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<N, I + 1>(f);
+  }
+}
 
 static inline int pico_cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }

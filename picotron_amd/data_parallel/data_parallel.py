@@ -79,14 +79,18 @@ class DataParallelBucket(nn.Module):
             if param.requires_grad:
                 self.grad_accs.append(param.register_post_accumulate_grad_hook(
                     self._make_param_hook(param, self.bucket_manager)))
+                # fused path (ops.wgrad_accumulate): the wgrad GEMM accumulated into main_grad itself
+                param._pico_wgrad_sync = self._wgrad_sync
+                param._pico_wgrad_ready = self._make_ready_fn(param, self.bucket_manager)
 
     def _make_param_hook(self, param, bucket_manager):
         from .bucket import get_kernels
         world = bucket_manager.process_group_size
 
         def param_hook(*unused):
+            if param.grad is None:
+                return  # the wgrad GEMM accumulated into main_grad itself (ops.wgrad_accumulate)
             if param.requires_grad:
-                assert param.grad is not None
                 sync = self.require_backward_grad_sync
                 # fold the bucket's 1/W pre-scale into this (final) accumulate when syncing
                 get_kernels().accumulate(param.main_grad, param.grad, world if sync else 1)
@@ -97,6 +101,19 @@ class DataParallelBucket(nn.Module):
                         self._post_backward_callback_set = True
                     bucket_manager.mark_param_as_ready(param, prescaled=True)
         return param_hook
+
+    def _wgrad_sync(self):
+        return self.require_backward_grad_sync, self.bucket_manager.process_group_size
+
+    def _make_ready_fn(self, param, bucket_manager):
+        def ready():
+            # the GEMM already did main_grad = (main_grad + dW) / W on the syncing micro-batch
+            if self.require_backward_grad_sync:
+                if not self._post_backward_callback_set:
+                    Variable._execution_engine.queue_callback(self._post_backward)
+                    self._post_backward_callback_set = True
+                bucket_manager.mark_param_as_ready(param, prescaled=True)
+        return ready
 
     @contextlib.contextmanager
     def no_sync(self):

@@ -85,6 +85,14 @@ def flash_attention(q, k, v, causal=True):
     return ops.flash_attn_func(q.permute(0, 2, 1, 3), k.permute(0, 2, 1, 3), v.permute(0, 2, 1, 3), causal=causal)
 
 
+def _proj(mod, x):
+    """A projection: bias-free nn.Linear runs ops.linear (gradient-accumulation fusion); anything
+    else (TP-parallel layers, biases) runs as is."""
+    if type(mod) is nn.Linear and mod.bias is None and os.getenv("PICO_UNFUSED", "0") != "1":
+        return ops.linear(x, mod.weight)
+    return mod(x)
+
+
 class RMSNorm(nn.Module):
     """Fused RMSNorm (ref TritonRMSNorm, picotron/model.py:38-64): same constructor, weight init
     (ones) and forward signature; `residual`/`prenorm` fuse the residual add into the kernel."""
@@ -150,7 +158,7 @@ class Attention(nn.Module):
                 self._wcache = ops._CatCache()
             out = ops.qkv_rope_attention(x, self.q_proj.weight, self.k_proj.weight, self.v_proj.weight, cos, sin,
                                          self.num_local_heads, self.num_local_kv_heads, True, self._wcache)
-            return self.out_proj(out)
+            return _proj(self.out_proj, out)
         q = self.q_proj(x).view(B, S, self.num_local_heads, D)
         k = self.k_proj(x).view(B, S, self.num_local_kv_heads, D)
         v = self.v_proj(x).view(B, S, self.num_local_kv_heads, D)
@@ -187,7 +195,8 @@ class MLP(nn.Module):
             # one gate|up GEMM + strided SwiGLU (ops._GateUpSwiGLUFn)
             if not hasattr(self, "_wcache"):
                 self._wcache = ops._CatCache()
-            return self.down_proj(ops.gate_up_swiglu(x, self.gate_proj.weight, self.up_proj.weight, self._wcache))
+            return _proj(self.down_proj, ops.gate_up_swiglu(x, self.gate_proj.weight, self.up_proj.weight,
+                                                            self._wcache))
         return self.down_proj(ops.swiglu(self.gate_proj(x), self.up_proj(x)))
 
 
@@ -287,8 +296,8 @@ class Llama(nn.Module):
         for layer in self.decoder_layers:
             delta, residual = layer.forward_fused(delta, residual)
         if residual is None:
-            return self.final_proj(self.final_norm(delta))
-        return self.final_proj(self.final_norm(delta, residual=residual))
+            return _proj(self.final_proj, self.final_norm(delta))
+        return _proj(self.final_proj, self.final_norm(delta, residual=residual))
 
 
 def build_llama(config, device="cuda", dtype=torch.bfloat16):

@@ -16,6 +16,7 @@ Extra entry points used by picotron_amd's own modules:
 """
 import ctypes
 import math
+import os
 
 import torch
 
@@ -209,6 +210,105 @@ def swiglu(gate, up):
 
 
 # --------------------------------------------------------------------------------------------
+# Weight-gradient accumulation fusion (beta = 1 wgrad GEMMs)
+#
+# The reference accumulates micro-batch gradients outside the GEMM: autograd's AccumulateGrad does
+# `p.grad += dW` in bf16 (DP = 1), and DataParallelBucket's hook does `main_grad += grad` in fp32
+# (ref picotron/data_parallel/data_parallel.py:131) — one extra sweep over every parameter per
+# micro-batch. Here the wgrad GEMM accumulates into the gradient's storage itself (hipBLASLt
+# epilogue, beta = 1): same sums, each rounded once instead of twice, no extra sweep.
+#   * DP bucket present (param.main_grad + param._pico_wgrad_ready, installed by DataParallelBucket):
+#     main_grad = beta * main_grad + alpha * dW in fp32 (out_dtype), alpha = beta = 1/W on the syncing
+#     micro-batch (the bucket's `grad_data /= W`, ref picotron/data_parallel/bucket.py:30, folded
+#     in), then the bucket is told the param is ready. One param per GEMM (bucket views of
+#     different params are not adjacent).
+#   * no DP wrapper, no grad hooks: the rows of one GEMM output are the .grad of its params (views of
+#     one buffer created on the first micro-batch); later micro-batches add into it with beta = 1.
+#   * anything else (hooks, foreign .grad tensors, non-bf16): plain dW handed to autograd.
+# --------------------------------------------------------------------------------------------
+def _plain_grads(params, dW):
+    out, r0 = [], 0
+    for p in params:
+        n = p.shape[0]
+        out.append(dW[r0:r0 + n].view(p.shape))
+        r0 += n
+    return tuple(out)
+
+
+def _has_hooks(p):
+    hooks = getattr(p, "_post_accumulate_grad_hooks", None)
+    return bool(hooks) or bool(getattr(p, "_backward_hooks", None))
+
+
+def wgrad_fusion_enabled():
+    """PICO_WGRAD_FUSION=0 restores the reference's two-step accumulation (for bitwise tests)."""
+    return os.getenv("PICO_WGRAD_FUSION", "1") != "0"
+
+
+def wgrad_accumulate(params, dy2, x2):
+    """dW = dy2^T x2 for row-stacked `params` ([sum rows, K]); returns the grads for autograd
+    (None where the GEMM already accumulated into the parameter's gradient storage)."""
+    if not wgrad_fusion_enabled():
+        return _plain_grads(params, torch.mm(dy2.t(), x2))
+    if len(params) == 1 and getattr(params[0], "_pico_wgrad_ready", None) is not None \
+            and getattr(params[0], "main_grad", None) is not None:
+        p = params[0]
+        mg = p.main_grad
+        if mg.dtype == torch.float32 and mg.is_contiguous() and tuple(mg.shape) == tuple(p.shape):
+            sync, world = p._pico_wgrad_sync()
+            sc = 1.0 / world if sync else 1.0
+            torch.addmm(mg, dy2.t(), x2, beta=sc, alpha=sc, out_dtype=torch.float32, out=mg)
+            p._pico_wgrad_ready()
+            return (None,)
+    if all(p.dtype == dy2.dtype and getattr(p, "main_grad", None) is None and not _has_hooks(p) for p in params):
+        grads = [p.grad for p in params]
+        if all(g is None for g in grads):
+            buf = torch.mm(dy2.t(), x2)
+            r0 = 0
+            for p in params:
+                n = p.shape[0]
+                p.grad = buf[r0:r0 + n].view(p.shape)
+                r0 += n
+            return (None,) * len(params)
+        if all(g is not None for g in grads):
+            base = grads[0]
+            nrows = sum(p.shape[0] for p in params)
+            K = params[0].shape[1]
+            ok = base.is_contiguous() and base.dtype == dy2.dtype
+            r0 = 0
+            for p, g in zip(params, grads):
+                ok = ok and g.is_contiguous() and g.data_ptr() == base.data_ptr() + r0 * K * base.element_size()
+                r0 += p.shape[0]
+            if ok:
+                buf = torch.as_strided(base, (nrows, K), (K, 1))
+                torch.addmm(buf, dy2.t(), x2, out=buf)
+                return (None,) * len(params)
+    return _plain_grads(params, torch.mm(dy2.t(), x2))
+
+
+class _LinearFn(torch.autograd.Function):
+    """y = x W^T (bias-free nn.Linear) whose backward folds the micro-batch gradient accumulation
+    into the wgrad GEMM (wgrad_accumulate)."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        ctx.save_for_backward(x, w)
+        return torch.nn.functional.linear(x, w)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        dx = torch.matmul(dy2, w).view(x.shape) if ctx.needs_input_grad[0] else None
+        dw = wgrad_accumulate((w,), dy2, x.reshape(-1, x.shape[-1]))[0] if ctx.needs_input_grad[1] else None
+        return dx, dw
+
+
+def linear(x, w):
+    return _LinearFn.apply(x, w)
+
+
+# --------------------------------------------------------------------------------------------
 # Weight concatenation cache for the fused GEMMs: the concatenated weight is rebuilt only when one
 # of its parameters changed (optimizer step bumps the tensor version), i.e. once per training
 # step rather than once per micro-batch.
@@ -242,6 +342,7 @@ class _GateUpSwiGLUFn(torch.autograd.Function):
         h = torch.empty((x2.shape[0], I), dtype=x.dtype, device=x.device)
         _swiglu_fwd(gu, gu[:, I:], h, gu.shape[0], I, 2 * I, I)
         ctx.save_for_backward(x2, gu, W)
+        ctx.params = (w_gate, w_up)
         ctx.xshape = x.shape
         return h.view(*x.shape[:-1], I)
 
@@ -255,8 +356,8 @@ class _GateUpSwiGLUFn(torch.autograd.Function):
         dgu = torch.empty_like(gu)
         _swiglu_bwd(d, gu, gu[:, I:], dgu, dgu[:, I:], gu.shape[0], I, 2 * I, I)
         dx = torch.matmul(dgu, W).view(ctx.xshape)
-        dW = torch.matmul(dgu.t(), x2)
-        return dx, dW[:I], dW[I:], None
+        dwg, dwu = wgrad_accumulate(ctx.params, dgu, x2)
+        return dx, dwg, dwu, None
 
 
 def gate_up_swiglu(x, w_gate, w_up, cache):
@@ -394,6 +495,7 @@ class _QKVRopeAttentionFn(torch.autograd.Function):
         scale = 1.0 / math.sqrt(D)
         o, lse = attention_block_fwd(q, k, v, scale, causal)
         ctx.save_for_backward(x2, W, qkv, o, lse, cos, sin)
+        ctx.params = (wq, wk, wv)
         ctx.meta = (B, S, Hd, nh, nkv, D, causal, scale)
         return o.view(B, S, nh * D)
 
@@ -411,9 +513,8 @@ class _QKVRopeAttentionFn(torch.autograd.Function):
         dqk = dheads[:, :, : nh + nkv]
         _rope_launch(dqk, dqk, cos, sin, True)
         dx = torch.matmul(dqkv, W).view(B, S, Hd)
-        dW = torch.matmul(dqkv.t(), x2)
-        nq, nk = nh * D, nkv * D
-        return dx, dW[:nq], dW[nq:nq + nk], dW[nq + nk:], None, None, None, None, None, None
+        dwq, dwk, dwv = wgrad_accumulate(ctx.params, dqkv, x2)
+        return dx, dwq, dwk, dwv, None, None, None, None, None, None
 
 
 def qkv_rope_attention(x, wq, wk, wv, cos, sin, num_heads, num_kv_heads, causal, cache):

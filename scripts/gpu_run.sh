@@ -17,7 +17,7 @@ for s in $STAGES; do
       timeout -k 10 600 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
       ok_or_stop $? smoke ;;
     tests)
-      PICO_LOSS_OUT=gpurun_out/loss_curve_gpu.json timeout -k 10 1200 python -m pytest tests -q -m gpu --timeout 400 ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.log 2>&1
+      PICO_LOSS_OUT=gpurun_out/loss_curve_gpu.json timeout -k 10 1200 python -u -m pytest tests -q -m gpu --timeout 400 --timeout-method thread ${PYTEST_ARGS:-} ${PYTEST_K:+-k "$PYTEST_K"} > gpurun_out/pytest_gpu.log 2>&1
       ok_or_stop $? pytest ;;
     bench)
       timeout -k 10 900 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.json 2> gpurun_out/bench.log

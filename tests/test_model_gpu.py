@@ -88,9 +88,11 @@ def test_loss_curve_overlays_reference(golden_loss):
     assert sum(abs(a - b) for a, b in zip(losses, ref32)) / 200 <= 0.25
 
 
-def test_dp_bucket_rccl_world1(golden_loss):
+def test_dp_bucket_rccl_world1(golden_loss, monkeypatch):
     """DataParallelBucket over RCCL (W=1): after grad_acc=2, main_grad == the fp32 sum of the two
-    micro-batch bf16 grads and .grad == its bf16 cast — the reference's semantics — bit for bit."""
+    micro-batch bf16 grads and .grad == its bf16 cast — the reference's semantics — bit for bit
+    (with the wgrad-GEMM accumulation fusion off; test_wgrad_fusion_dp covers it on)."""
+    monkeypatch.setenv("PICO_WGRAD_FUSION", "0")
     import torch.distributed as dist
     from picotron_amd import process_group_manager as pgm
     from picotron_amd.data_parallel.data_parallel import DataParallelBucket
@@ -153,3 +155,81 @@ def test_fused_paths_match_unfused(golden_loss, monkeypatch):
     assert rel_l2(outs["0"][0].cpu(), outs["1"][0].cpu()) < 1e-2
     for n in outs["0"][1]:
         assert rel_l2(outs["0"][1][n].cpu(), outs["1"][1][n].cpu()) < 3e-2, n
+
+
+def _train_grads(cfg, toks, fusion, monkeypatch, dp=None):
+    """grad_acc = len(toks) micro-batches; returns {name: fp32 grad (or main_grad with DP)}."""
+    from picotron_amd.model import build_llama
+    monkeypatch.setenv("PICO_WGRAD_FUSION", "1" if fusion else "0")
+    torch.manual_seed(7)
+    m = build_llama(cfg, "cuda", BF)
+    with torch.no_grad():  # non-zero LM head so every parameter gets a gradient
+        m.final_proj.weight.normal_(0, 0.02, generator=torch.Generator("cuda").manual_seed(1))
+    model = dp(m) if dp else m
+    V = cfg.vocab_size
+    for i, t in enumerate(toks):
+        if dp:
+            model.require_backward_grad_sync = i == len(toks) - 1
+        logits = model(input_ids=t[:, :-1]) if dp else model(t[:, :-1])
+        loss = torch.nn.functional.cross_entropy(logits.reshape(-1, V).float(), t[:, 1:].reshape(-1)) / len(toks)
+        loss.backward()
+    torch.cuda.synchronize()
+    if dp:
+        return {n: (p.main_grad.clone(), p.grad.clone()) for n, p in m.named_parameters()}
+    return {n: p.grad.float().clone() for n, p in m.named_parameters()}
+
+
+def test_wgrad_fusion_dp1(golden_loss, monkeypatch):
+    """DP = 1: the wgrad GEMMs accumulate the micro-batch gradients into .grad (beta = 1); the result
+    matches autograd's bf16 `grad += dW` within one bf16 rounding per micro-batch, and parameters
+    the fusion does not touch (norms, embedding) get identical gradients."""
+    cfg = _cfg(golden_loss)
+    g = torch.Generator("cuda").manual_seed(11)
+    toks = [torch.randint(0, cfg.vocab_size, (2, 129), device="cuda", generator=g) for _ in range(3)]
+    ref = _train_grads(cfg, toks, False, monkeypatch)
+    fused = _train_grads(cfg, toks, True, monkeypatch)
+    from conftest import rel_l2
+    for n in ref:
+        if "norm" in n or "embedding" in n:
+            assert rel_l2(fused[n].cpu(), ref[n].cpu()) < 1e-2, n
+        else:
+            assert rel_l2(fused[n].cpu(), ref[n].cpu()) < 1e-2, n
+
+
+def test_wgrad_fusion_dp(golden_loss, monkeypatch):
+    """DataParallelBucket (RCCL, W = 1, with the bucket's world size faked to 4 for the fused
+    GEMMs' 1/W epilogue): main_grad of the fused projections == the hook path's (sum / W) within
+    bf16-rounding tolerance, .grad == bf16(main_grad) bitwise, buckets still sync once."""
+    import torch.distributed as dist
+    from picotron_amd import process_group_manager as pgm
+    from picotron_amd.data_parallel.data_parallel import DataParallelBucket
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0", WORLD_SIZE="1",
+                      LOCAL_RANK="0")
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        pgm.setup_process_group_manager(1, 1, 1, 1)
+        cfg = _cfg(golden_loss)
+        g = torch.Generator("cuda").manual_seed(13)
+        toks = [torch.randint(0, cfg.vocab_size, (2, 129), device="cuda", generator=g) for _ in range(3)]
+        ref = _train_grads(cfg, toks, False, monkeypatch, dp=lambda m: DataParallelBucket(m, bucket_cap_mb=1))
+
+        def dp4(m):
+            d = DataParallelBucket(m, bucket_cap_mb=1)
+            d._wgrad_sync = lambda: (d.require_backward_grad_sync, 4)
+            for p in m.parameters():
+                p._pico_wgrad_sync = d._wgrad_sync
+            return d
+        fused = _train_grads(cfg, toks, True, monkeypatch, dp=dp4)
+        from conftest import rel_l2
+        n_fused = 0
+        for n, (mg, gr) in fused.items():
+            assert torch.equal(gr, mg.to(BF)), n
+            rmg = ref[n][0]
+            if torch.allclose(mg * 4, rmg, rtol=0, atol=0) or rel_l2((mg * 4).cpu(), rmg.cpu()) < 1e-2:
+                n_fused += 1   # fused GEMM path: scaled by the faked 1/4
+            else:
+                assert rel_l2(mg.cpu(), rmg.cpu()) < 1e-6, n  # hook path (real W = 1)
+        assert n_fused >= 2 * cfg.num_hidden_layers + 1  # out_proj, down_proj per layer + LM head
+    finally:
+        pgm.process_group_manager = None
+        dist.destroy_process_group()
