@@ -76,6 +76,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--cpu-seq", type=int, default=256)
+    ap.add_argument("--graphs", type=int, default=1,
+                    help="replay non-syncing micro-batches as a HIP graph (1) or run them eagerly (0)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -96,7 +98,7 @@ def main():
     from picotron_amd.data import SyntheticDataLoader
     from picotron_amd.data_parallel.data_parallel import DataParallelBucket
     from picotron_amd.model import build_llama, smollm_1_7b
-    from picotron_amd.train import get_mfu, train_step
+    from picotron_amd.train import MicroBatchGraph, get_mfu, train_step
 
     L.load()
     pgm.setup_process_group_manager(tp_size=1, cp_size=1, pp_size=1, dp_size=world)
@@ -112,9 +114,19 @@ def main():
                                  num_batches=args.grad_acc, device=device)
     log(f"[rank {rank}] model {num_params / 1e9:.3f}B params built in {time.time() - t0:.1f}s")
 
+    def zero_grads():
+        for p in model.parameters():
+            if p.grad is not None:
+                p.grad.zero_()
+        if hasattr(model, "bucket_manager"):
+            model.bucket_manager.reset()
+
+    graphs = MicroBatchGraph(model, args.grad_acc, zero_grads) if args.graphs else None
+
     def step():
-        opt.zero_grad()
-        loss = train_step(model, loader, device)
+        # graphs: gradient buffers must persist (zeroed in place); eager: the reference's set_to_none
+        opt.zero_grad(set_to_none=graphs is None)
+        loss = train_step(model, loader, device, graphs=graphs)
         opt.step()
         if hasattr(model, "reset"):
             model.reset()
@@ -127,7 +139,10 @@ def main():
 
     kernel_ids = [L.K_ATTN_FWD, L.K_ATTN_BWD, L.K_ATTN_BWD_PRE, L.K_ATTN_BWD_DQ, L.K_RMSNORM_FWD, L.K_RMSNORM_BWD,
                   L.K_RMSNORM_DW, L.K_ROPE, L.K_SWIGLU_FWD, L.K_SWIGLU_BWD, L.K_GRAD_ACCUM, L.K_CAST]
-    if not args.no_kernel_timing:
+    # Per-launch HIP events cannot ride inside a graph replay, so with graphs the kernels are timed
+    # over one extra eagerly launched step right after the timed region (same shapes, same stream).
+    kernel_timing_live = not args.graphs
+    if not args.no_kernel_timing and kernel_timing_live:
         cap = args.steps * args.grad_acc * (args.layers * 4 + 8) + 16
         for k in kernel_ids:
             L.prof_enable(k, cap)
@@ -146,6 +161,13 @@ def main():
     elapsed = float(t.item())
 
     kernels = {}
+    if not args.no_kernel_timing and not kernel_timing_live:
+        cap = args.grad_acc * (args.layers * 4 + 8) + 16
+        for k in kernel_ids:
+            L.prof_enable(k, cap)
+        opt.zero_grad(set_to_none=False)
+        train_step(model, loader, device, graphs=None)
+        torch.cuda.synchronize()
     if not args.no_kernel_timing:
         for k in kernel_ids:
             tot, n = L.prof_collect(k)
@@ -176,7 +198,9 @@ def main():
             achieved, peak, u = amount / avg_s / 1e9, HBM_PEAK_GBS, "GB/s"
         roofline = {"kernel": dom, "bound": bound, "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": u,
                     "frac": round(achieved / peak, 4), "traffic": None,
-                    "work_per_launch": amount, "avg_launch_us": round(kernels[dom]["avg_us"], 2)}
+                    "work_per_launch": amount, "avg_launch_us": round(kernels[dom]["avg_us"], 2),
+                    "timed_over": ("the timed region" if kernel_timing_live else
+                                   "one eager step right after the timed region (graph replays carry no per-launch events)")}
         for name, v in kernels.items():
             kk = [k for k in kernel_ids if L.KERNEL_NAMES[k] == name][0]
             w = kernel_work(kk, cfg, MBS, SEQ)

@@ -21,6 +21,8 @@
  *                                                                      (ref picotron/data_parallel/bucket.py:30)
  *   pico_cast_f32_bf16        <- p.grad = p.main_grad.to(p.dtype)    (ref picotron/data_parallel/data_parallel.py:165)
  *   pico_scale_f32            <- grad_data /= process_group_size     (ref picotron/data_parallel/bucket.py:30)
+ *   pico_embedding_bwd        <- backward of F.embedding (ref picotron/model.py:223-224) + the micro-batch
+ *                                 gradient accumulation (data_parallel.py:131 / autograd's grad += dW)
  *
  * Conventions: all pointers are device pointers allocated by the caller (kernels never
  * allocate); bf16 tensors are passed as raw 16-bit storage; `stream` is a hipStream_t
@@ -56,7 +58,8 @@ enum {
   PICO_K_CAST = 12,
   PICO_K_SCALE = 13,
   PICO_K_ATTN_MERGE = 14,
-  PICO_K_COUNT = 15
+  PICO_K_EMBEDDING_BWD = 15,
+  PICO_K_COUNT = 16
 };
 
 int pico_abi_version(void);
@@ -147,6 +150,13 @@ int pico_grad_accum(float* main_grad, const void* grad, int64_t n, float divide_
 int pico_scale_f32(float* buf, int64_t n, float divide_by, void* stream);
 /* dst[i] = bf16(src[i]) (round to nearest even) */
 int pico_cast_f32_bf16(const float* src, void* dst, int64_t n, void* stream);
+
+/* ---- token embedding backward (deterministic, graph-safe) ----
+ * sorted_ids / sorted_pos: the n_tokens token ids stable-sorted ascending and their positions
+ * (int64, device). dy: [n_tokens, dim] bf16. grad: [vocab, dim] bf16 (grad_is_f32 = 0) or fp32;
+ * for every id present: grad[id] = (grad[id] + sum of its dy rows in position order) * scale. */
+int pico_embedding_bwd(const int64_t* sorted_ids, const int64_t* sorted_pos, const void* dy, void* grad,
+                       int64_t n_tokens, int64_t dim, int grad_is_f32, float scale, void* stream);
 
 #ifdef __cplusplus
 }

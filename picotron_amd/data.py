@@ -66,16 +66,18 @@ class SyntheticDataLoader:
     def __iter__(self):
         return self
 
-    def __next__(self):
-        if self.num_batches is None:
-            toks = self._make()
-        else:
-            if len(self._cache) < self.num_batches:
-                self._cache.append(self._make())
-            toks = self._cache[self._i % self.num_batches]
-        self._i += 1
+    def _device_batch(self, toks):
         batch = self.collate(toks)
         if self.device != "cpu":
             for k in ("input_ids", "target_ids", "position_ids"):
                 batch[k] = batch[k].to(self.device, non_blocking=True)
         return batch
+
+    def __next__(self):
+        self._i += 1
+        if self.num_batches is None:
+            return self._device_batch(self._make())
+        # a fixed cycle of micro-batches: generated once and kept resident on the device
+        if len(self._cache) < self.num_batches:
+            self._cache.append(self._device_batch(self._make()))
+        return dict(self._cache[(self._i - 1) % self.num_batches])

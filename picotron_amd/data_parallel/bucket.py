@@ -119,7 +119,8 @@ class Bucket:
                 _kernels.cast(self.grad_data, self.grad_out)
 
     def mark_param_as_ready(self, param: torch.nn.Parameter, prescaled: bool = False) -> None:
-        assert param in self.params and param not in self.params_with_grad_ready
+        assert param in self.params and param not in self.params_with_grad_ready, \
+            f"param {tuple(param.shape)} marked ready twice (or foreign)"
         self.params_with_grad_ready.add(param)
         if prescaled:
             self.n_prescaled += 1

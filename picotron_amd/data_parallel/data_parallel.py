@@ -88,8 +88,11 @@ class DataParallelBucket(nn.Module):
         world = bucket_manager.process_group_size
 
         def param_hook(*unused):
-            if param.grad is None:
-                return  # the wgrad GEMM accumulated into main_grad itself (ops.wgrad_accumulate)
+            if getattr(param, "_pico_fused_pending", False):
+                # the wgrad GEMM / embedding kernel accumulated into main_grad itself and already
+                # marked the param ready (ops.wgrad_accumulate); AccumulateGrad got no gradient
+                param._pico_fused_pending = False
+                return
             if param.requires_grad:
                 sync = self.require_backward_grad_sync
                 # fold the bucket's 1/W pre-scale into this (final) accumulate when syncing
@@ -108,6 +111,7 @@ class DataParallelBucket(nn.Module):
     def _make_ready_fn(self, param, bucket_manager):
         def ready():
             # the GEMM already did main_grad = (main_grad + dW) / W on the syncing micro-batch
+            param._pico_fused_pending = True
             if self.require_backward_grad_sync:
                 if not self._post_backward_callback_set:
                     Variable._execution_engine.queue_callback(self._post_backward)

@@ -154,10 +154,8 @@ class Attention(nn.Module):
         D = self.head_dim
         if self._fusable():
             # one q|k|v GEMM, RoPE in place on q|k, attention on strided views (ops._QKVRopeAttentionFn)
-            if not hasattr(self, "_wcache"):
-                self._wcache = ops._CatCache()
             out = ops.qkv_rope_attention(x, self.q_proj.weight, self.k_proj.weight, self.v_proj.weight, cos, sin,
-                                         self.num_local_heads, self.num_local_kv_heads, True, self._wcache)
+                                         self.num_local_heads, self.num_local_kv_heads, True)
             return _proj(self.out_proj, out)
         q = self.q_proj(x).view(B, S, self.num_local_heads, D)
         k = self.k_proj(x).view(B, S, self.num_local_kv_heads, D)
@@ -193,10 +191,7 @@ class MLP(nn.Module):
         if (os.getenv("PICO_UNFUSED", "0") != "1" and type(self.gate_proj) is nn.Linear
                 and type(self.up_proj) is nn.Linear and self.gate_proj.bias is None and self.up_proj.bias is None):
             # one gate|up GEMM + strided SwiGLU (ops._GateUpSwiGLUFn)
-            if not hasattr(self, "_wcache"):
-                self._wcache = ops._CatCache()
-            return _proj(self.down_proj, ops.gate_up_swiglu(x, self.gate_proj.weight, self.up_proj.weight,
-                                                            self._wcache))
+            return _proj(self.down_proj, ops.gate_up_swiglu(x, self.gate_proj.weight, self.up_proj.weight))
         return self.down_proj(ops.swiglu(self.gate_proj(x), self.up_proj(x)))
 
 
@@ -250,6 +245,8 @@ class Embedding(nn.Module):
         torch.nn.init.normal_(self.weight, mean=0.0, std=1.0)
 
     def forward(self, x):
+        if self.padding_idx is None and x.is_cuda:
+            return ops.embedding(x, self.weight)  # deterministic, graph-safe backward
         return F.embedding(x, self.weight, self.padding_idx)
 
 

@@ -276,14 +276,66 @@ def wgrad_accumulate(params, dy2, x2):
             K = params[0].shape[1]
             ok = base.is_contiguous() and base.dtype == dy2.dtype
             r0 = 0
+            sp = base.untyped_storage().data_ptr()
             for p, g in zip(params, grads):
-                ok = ok and g.is_contiguous() and g.data_ptr() == base.data_ptr() + r0 * K * base.element_size()
+                ok = ok and g.is_contiguous() and g.untyped_storage().data_ptr() == sp and \
+                    g.data_ptr() == base.data_ptr() + r0 * K * base.element_size()
                 r0 += p.shape[0]
             if ok:
                 buf = torch.as_strided(base, (nrows, K), (K, 1))
                 torch.addmm(buf, dy2.t(), x2, out=buf)
                 return (None,) * len(params)
     return _plain_grads(params, torch.mm(dy2.t(), x2))
+
+
+def _embedding_bwd_into(grad, ids, dy, scale):
+    flat = ids.reshape(-1)
+    sids, spos = torch.sort(flat, stable=True)
+    dy2 = dy.reshape(-1, dy.shape[-1])
+    if not dy2.is_contiguous():
+        dy2 = dy2.contiguous()
+    _lib.check(_lib.load().pico_embedding_bwd(_lib.ptr(sids), _lib.ptr(spos), _lib.ptr(dy2), _lib.ptr(grad),
+                                              flat.numel(), dy2.shape[1], 1 if grad.dtype == torch.float32 else 0,
+                                              float(scale), _lib.stream_of(dy2)), "pico_embedding_bwd")
+
+
+class _EmbeddingFn(torch.autograd.Function):
+    """F.embedding whose backward (pico_embedding_bwd) adds the touched rows straight into the
+    gradient storage — .grad (DP = 1), or the fp32 main_grad with 1/W on the syncing micro-batch
+    (DataParallelBucket) — instead of materialising a dense [V, H] gradient (ref
+    picotron/model.py:223-224). Deterministic and HIP-graph safe."""
+
+    @staticmethod
+    def forward(ctx, ids, w):
+        ctx.save_for_backward(ids)
+        ctx.w = w
+        return torch.nn.functional.embedding(ids, w)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (ids,) = ctx.saved_tensors
+        w = ctx.w
+        if getattr(w, "_pico_wgrad_ready", None) is not None and getattr(w, "main_grad", None) is not None:
+            sync, world = w._pico_wgrad_sync()
+            _embedding_bwd_into(w.main_grad, ids, dy, 1.0)
+            if sync and world != 1:  # the bucket's grad_data /= W covers every row, touched or not
+                w.main_grad.mul_(1.0 / world)
+            w._pico_wgrad_ready()
+            return None, None
+        if getattr(w, "main_grad", None) is None and not _has_hooks(w):
+            if w.grad is None:
+                w.grad = torch.zeros_like(w)
+            _embedding_bwd_into(w.grad, ids, dy, 1.0)
+            return None, None
+        g = torch.zeros_like(w)
+        _embedding_bwd_into(g, ids, dy, 1.0)
+        return None, g
+
+
+def embedding(ids, w):
+    if not wgrad_fusion_enabled():
+        return torch.nn.functional.embedding(ids, w)
+    return _EmbeddingFn.apply(ids, w)
 
 
 class _LinearFn(torch.autograd.Function):
@@ -309,22 +361,33 @@ def linear(x, w):
 
 
 # --------------------------------------------------------------------------------------------
-# Weight concatenation cache for the fused GEMMs: the concatenated weight is rebuilt only when one
-# of its parameters changed (optimizer step bumps the tensor version), i.e. once per training
-# step rather than once per micro-batch.
+# Stacked weights for the fused GEMMs: [Wq; Wk; Wv] and [Wg; Wu] are one buffer whose row blocks ARE
+# the parameters (p.data re-pointed in place on first use, or after a .to() moved them), so the
+# fused GEMM reads the parameters themselves: no concatenated copy, nothing to refresh after the
+# optimizer step, and the parameter objects, names and registration order are unchanged.
 # --------------------------------------------------------------------------------------------
-class _CatCache:
-    def __init__(self):
-        self.key = None
-        self.value = None
-
-    def get(self, ws):
-        key = tuple((w.data_ptr(), w._version, tuple(w.shape)) for w in ws)
-        if key != self.key:
-            with torch.no_grad():
-                self.value = torch.cat([w.detach() for w in ws], 0)
-            self.key = key
-        return self.value
+def stacked_weight(ws):
+    K = ws[0].shape[1]
+    N = sum(w.shape[0] for w in ws)
+    base = ws[0]
+    ok = all(w.is_contiguous() and w.dtype == base.dtype and w.device == base.device and w.shape[1] == K
+             for w in ws)
+    sp = base.untyped_storage().data_ptr()
+    off = 0
+    for w in ws:
+        ok = ok and w.untyped_storage().data_ptr() == sp and \
+            w.data_ptr() == base.data_ptr() + off * K * base.element_size()
+        off += w.shape[0]
+    if not ok:
+        with torch.no_grad():
+            buf = torch.cat([w.detach() for w in ws], 0)
+        r0 = 0
+        for w in ws:
+            n = w.shape[0]
+            w.data = buf[r0:r0 + n]
+            r0 += n
+        base = ws[0]
+    return base.detach().as_strided((N, K), (K, 1))
 
 
 class _GateUpSwiGLUFn(torch.autograd.Function):
@@ -333,10 +396,10 @@ class _GateUpSwiGLUFn(torch.autograd.Function):
     so x's gradient is one GEMM (no sum of two dgrads) and the weight gradient one GEMM."""
 
     @staticmethod
-    def forward(ctx, x, w_gate, w_up, cache):
+    def forward(ctx, x, w_gate, w_up):
         _need(x, "x")
         I = w_gate.shape[0]
-        W = cache.get((w_gate, w_up))
+        W = stacked_weight((w_gate, w_up))
         x2 = x.reshape(-1, x.shape[-1])
         gu = torch.matmul(x2, W.t())  # [T, 2I]
         h = torch.empty((x2.shape[0], I), dtype=x.dtype, device=x.device)
@@ -357,11 +420,11 @@ class _GateUpSwiGLUFn(torch.autograd.Function):
         _swiglu_bwd(d, gu, gu[:, I:], dgu, dgu[:, I:], gu.shape[0], I, 2 * I, I)
         dx = torch.matmul(dgu, W).view(ctx.xshape)
         dwg, dwu = wgrad_accumulate(ctx.params, dgu, x2)
-        return dx, dwg, dwu, None
+        return dx, dwg, dwu
 
 
-def gate_up_swiglu(x, w_gate, w_up, cache):
-    return _GateUpSwiGLUFn.apply(x, w_gate, w_up, cache)
+def gate_up_swiglu(x, w_gate, w_up):
+    return _GateUpSwiGLUFn.apply(x, w_gate, w_up)
 
 
 # --------------------------------------------------------------------------------------------
@@ -480,11 +543,11 @@ class _QKVRopeAttentionFn(torch.autograd.Function):
     dW = dqkv^T x (one GEMM, rows = dWq | dWk | dWv)."""
 
     @staticmethod
-    def forward(ctx, x, wq, wk, wv, cos, sin, nh, nkv, causal, cache):
+    def forward(ctx, x, wq, wk, wv, cos, sin, nh, nkv, causal):
         _need(x, "x")
         B, S, Hd = x.shape
         D = wq.shape[0] // nh
-        W = cache.get((wq, wk, wv))
+        W = stacked_weight((wq, wk, wv))
         N = W.shape[0]
         x2 = x.reshape(B * S, Hd)
         qkv = torch.matmul(x2, W.t())  # [T, (nh + 2 nkv) D]
@@ -514,14 +577,14 @@ class _QKVRopeAttentionFn(torch.autograd.Function):
         _rope_launch(dqk, dqk, cos, sin, True)
         dx = torch.matmul(dqkv, W).view(B, S, Hd)
         dwq, dwk, dwv = wgrad_accumulate(ctx.params, dqkv, x2)
-        return dx, dwq, dwk, dwv, None, None, None, None, None, None
+        return dx, dwq, dwk, dwv, None, None, None, None, None
 
 
-def qkv_rope_attention(x, wq, wk, wv, cos, sin, num_heads, num_kv_heads, causal, cache):
+def qkv_rope_attention(x, wq, wk, wv, cos, sin, num_heads, num_kv_heads, causal):
     """Fused attention block (projections + RoPE + flash attention); see _QKVRopeAttentionFn."""
     D = wq.shape[0] // num_heads
     return _QKVRopeAttentionFn.apply(x, wq, wk, wv, cos[:, : D // 2], sin[:, : D // 2], num_heads, num_kv_heads,
-                                     causal, cache)
+                                     causal)
 
 
 def _attention_bwd_into(dout, q, k, v, o, lse, softmax_scale, causal, dq, dk, dv):

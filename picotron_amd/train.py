@@ -13,28 +13,95 @@ from . import process_group_manager as pgm
 MI355X_BF16_PEAK = 256 * 4096 * 2.4e9
 
 
-def train_step(model, data_loader, device):
+def _micro_batch(model, input_ids, target_ids, grad_acc_steps):
+    outputs = model(input_ids=input_ids)
+    batch_size, seq_len = input_ids.shape
+    outputs = outputs.view(seq_len * batch_size, -1)
+    loss = F.cross_entropy(outputs, target_ids.reshape(-1), reduction="mean") / grad_acc_steps
+    loss.backward()
+    return loss.detach()
+
+
+def train_step(model, data_loader, device, graphs=None):
     """ref train.py:29-55: grad-accumulation loop, DP sync only on the last micro-batch,
-    mean CE / grad_acc_steps, returns the accumulated (python float) loss."""
-    acc_loss = 0.0
+    mean CE / grad_acc_steps, returns the accumulated (python float) loss.
+    `graphs` (a MicroBatchGraph) replays the micro-batches that do not sync DP gradients."""
     m = pgm.process_group_manager
-    requires_grad_sync = m is not None and m.cp_dp_world_size > 1
+    # the reference toggles DP sync only when cp_dp_world_size > 1; a DP wrapper at W = 1 is toggled
+    # too (identical sums: all-reducing once at the end == every micro-batch when W = 1)
+    requires_grad_sync = (m is not None and m.cp_dp_world_size > 1) or hasattr(model, "require_backward_grad_sync")
     losses = []
-    for i in range(data_loader.grad_acc_steps):
+    n = data_loader.grad_acc_steps
+    for i in range(n):
         batch = next(data_loader)
         input_ids = batch["input_ids"].to(device)
         target_ids = batch["target_ids"].to(device)
+        sync = requires_grad_sync and i == n - 1
         if requires_grad_sync:
-            model.require_backward_grad_sync = (i == data_loader.grad_acc_steps - 1)
-        outputs = model(input_ids=input_ids)
-        batch_size, seq_len = input_ids.shape
-        outputs = outputs.view(seq_len * batch_size, -1)
-        loss = F.cross_entropy(outputs, target_ids.reshape(-1), reduction="mean") / data_loader.grad_acc_steps
-        loss.backward()
-        losses.append(loss.detach())
+            model.require_backward_grad_sync = sync
+        if graphs is not None and not sync:  # syncing micro-batches launch RCCL from hooks: eager
+            graphs.replay(input_ids, target_ids)
+        else:
+            losses.append(_micro_batch(model, input_ids, target_ids, n))
+    if graphs is not None:
+        losses.append(graphs.take_loss())
     # one host sync per step instead of one per micro-batch (ref :53 calls .item() each time)
-    acc_loss = float(torch.stack(losses).float().sum().item()) if losses else 0.0
-    return acc_loss
+    return float(torch.stack(losses).float().sum().item()) if losses else 0.0
+
+
+class MicroBatchGraph:
+    """A training micro-batch (forward, mean CE / grad_acc, backward) captured once as a HIP graph
+    and replayed: the ~330 kernels of a SmolLM-1.7B micro-batch then launch back to back instead of
+    paying a host dispatch gap each. Inputs are copied into static buffers, the loss is accumulated
+    on the device, and gradients accumulate into persistent buffers — so between steps gradients
+    must be zeroed in place (`optimizer.zero_grad(set_to_none=False)`), never dropped. Micro-batches
+    that sync DP gradients (RCCL all-reduces launched from hooks) are not replayed; train_step runs
+    them eagerly. Capture happens on the first replay: two eager warm-up micro-batches on a side
+    stream, then the capture; their effects on gradients / the loss are undone (zeroed), so call it
+    at the start of a step (grads zero)."""
+
+    def __init__(self, model, grad_acc_steps, zero_grads):
+        self.model = model
+        self.n = grad_acc_steps
+        self.zero_grads = zero_grads  # callable zeroing every gradient buffer in place
+        self.graph = None
+        self.inp = self.tgt = None
+        self.loss_acc = None
+
+    def _fwd_bwd(self):
+        self.loss_acc += _micro_batch(self.model, self.inp, self.tgt, self.n)
+
+    def _capture(self, input_ids, target_ids):
+        self.inp = input_ids.clone()
+        self.tgt = target_ids.clone()
+        self.loss_acc = torch.zeros((), dtype=torch.float32, device=input_ids.device)
+        side = torch.cuda.Stream(device=input_ids.device)
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(2):
+                self._fwd_bwd()
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self._fwd_bwd()
+        torch.cuda.synchronize()
+        self.zero_grads()
+        self.loss_acc.zero_()
+
+    def replay(self, input_ids, target_ids):
+        if self.graph is None:
+            self._capture(input_ids, target_ids)
+        self.inp.copy_(input_ids)
+        self.tgt.copy_(target_ids)
+        self.graph.replay()
+
+    def take_loss(self):
+        if self.loss_acc is None:
+            return torch.zeros(())
+        out = self.loss_acc.clone()
+        self.loss_acc.zero_()
+        return out
 
 
 def get_mfu(tokens_per_second_per_gpu, num_params, model_config, theoretical_flops=MI355X_BF16_PEAK):

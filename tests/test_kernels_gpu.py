@@ -310,3 +310,32 @@ def test_grad_accum_and_cast_bit_exact():
     ref = v.clone().add_(gg[3:803])
     K.accumulate(v, gg[3:803], 1)
     assert torch.equal(v, ref)
+
+
+# ------------------------------------------------------------------------------------------ embedding
+@pytest.mark.parametrize("grad_dtype", [torch.bfloat16, torch.float32])
+def test_embedding_bwd_matches_dense(grad_dtype):
+    """pico_embedding_bwd (stable sort + one workgroup per id run) == the dense backward of
+    F.embedding accumulated into an existing gradient, incl. repeated ids and the 1/W scale; and it
+    is deterministic (bitwise equal across calls)."""
+    from picotron_amd.ops import _embedding_bwd_into
+    torch.manual_seed(1)
+    V, H, B, S = 512, 256, 3, 100
+    ids = torch.randint(0, V // 4, (B, S), device=DEV)  # many repeats
+    dy = torch.randn(B, S, H, dtype=BF, device=DEV)
+    g0 = torch.randn(V, H, dtype=grad_dtype, device=DEV)
+    dense = torch.zeros(V, H, dtype=torch.float64, device=DEV)
+    dense.index_add_(0, ids.reshape(-1), dy.reshape(-1, H).double())
+    scale = 0.25 if grad_dtype == torch.float32 else 1.0
+    touched = torch.zeros(V, dtype=torch.bool, device=DEV)
+    touched[ids.reshape(-1)] = True
+    want = g0.double() + dense
+    want[touched] *= scale  # only the rows of ids present are rewritten (and scaled)
+    got = g0.clone()
+    _embedding_bwd_into(got, ids, dy, scale)
+    tol = 1e-6 if grad_dtype == torch.float32 else 8e-3
+    assert rel_l2(got.cpu(), want.cpu()) < tol
+    assert torch.equal(got[~touched], g0[~touched])
+    again = g0.clone()
+    _embedding_bwd_into(again, ids, dy, scale)
+    assert torch.equal(again, got)

@@ -233,3 +233,93 @@ def test_wgrad_fusion_dp(golden_loss, monkeypatch):
     finally:
         pgm.process_group_manager = None
         dist.destroy_process_group()
+
+
+def test_graph_replay_matches_eager(golden_loss):
+    """MicroBatchGraph (HIP-graph replay of forward + CE + backward) gives the eager loop's loss and
+    gradients bit for bit over a 3-micro-batch step, and a second step after an optimizer update."""
+    from picotron_amd.data import SyntheticDataLoader
+    from picotron_amd.model import build_llama
+    from picotron_amd.train import MicroBatchGraph, train_step
+    cfg = _cfg(golden_loss)
+    results = []
+    for use_graph in (False, True):
+        torch.manual_seed(7)
+        m = build_llama(cfg, "cuda", BF)
+        with torch.no_grad():
+            m.final_proj.weight.normal_(0, 0.02, generator=torch.Generator("cuda").manual_seed(1))
+        opt = torch.optim.AdamW(m.parameters(), lr=1e-3)
+        loader = SyntheticDataLoader(2, 128, 3, cfg.vocab_size, seed=5, kind="uniform", num_batches=3, device="cuda")
+
+        def zero():
+            for p in m.parameters():
+                if p.grad is not None:
+                    p.grad.zero_()
+        g = MicroBatchGraph(m, 3, zero) if use_graph else None
+        losses, grads = [], None
+        for step in range(2):
+            opt.zero_grad(set_to_none=False)
+            losses.append(train_step(m, loader, "cuda", graphs=g))
+            if step == 0:
+                grads = {n: p.grad.clone() for n, p in m.named_parameters()}
+            opt.step()
+        torch.cuda.synchronize()
+        results.append((losses, grads, {n: p.detach().clone() for n, p in m.named_parameters()}))
+    (l0, g0, p0), (l1, g1, p1) = results
+    assert l0 == l1, (l0, l1)
+    for n in g0:
+        assert torch.equal(g0[n], g1[n]), n
+        assert torch.equal(p0[n], p1[n]), n
+
+
+def test_graph_replay_with_dp_bucket(golden_loss):
+    """DataParallelBucket (RCCL, W = 1) + MicroBatchGraph: the non-syncing micro-batches replay as a
+    graph (their DP hooks' accumulates are captured), the syncing one runs eagerly; main_grad, .grad
+    and the updated parameters equal the all-eager loop bit for bit, over two steps."""
+    import torch.distributed as dist
+    from picotron_amd import process_group_manager as pgm
+    from picotron_amd.data import SyntheticDataLoader
+    from picotron_amd.data_parallel.data_parallel import DataParallelBucket
+    from picotron_amd.model import build_llama
+    from picotron_amd.train import MicroBatchGraph, train_step
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0", WORLD_SIZE="1",
+                      LOCAL_RANK="0")
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        pgm.setup_process_group_manager(1, 1, 1, 1)
+        cfg = _cfg(golden_loss)
+        res = []
+        for use_graph in (False, True):
+            torch.manual_seed(7)
+            m = build_llama(cfg, "cuda", BF)
+            with torch.no_grad():
+                m.final_proj.weight.normal_(0, 0.02, generator=torch.Generator("cuda").manual_seed(1))
+            ddp = DataParallelBucket(m, bucket_cap_mb=1)
+            opt = torch.optim.AdamW(ddp.parameters(), lr=1e-3)
+            loader = SyntheticDataLoader(2, 128, 3, cfg.vocab_size, seed=5, num_batches=3, device="cuda")
+
+            def zero():
+                for p in m.parameters():
+                    if p.grad is not None:
+                        p.grad.zero_()
+                ddp.bucket_manager.reset()
+            g = MicroBatchGraph(ddp, 3, zero) if use_graph else None
+            losses, snap = [], None
+            for step in range(2):
+                opt.zero_grad(set_to_none=not use_graph)
+                losses.append(train_step(ddp, loader, "cuda", graphs=g))
+                if step == 0:
+                    snap = {n: (p.main_grad.clone(), p.grad.clone()) for n, p in m.named_parameters()}
+                opt.step()
+                ddp.reset()
+            torch.cuda.synchronize()
+            res.append((losses, snap, {n: p.detach().clone() for n, p in m.named_parameters()}))
+        (l0, s0, p0), (l1, s1, p1) = res
+        assert l0 == l1, (l0, l1)
+        for n in s0:
+            assert torch.equal(s0[n][0], s1[n][0]), n
+            assert torch.equal(s0[n][1], s1[n][1]), n
+            assert torch.equal(p0[n], p1[n]), n
+    finally:
+        pgm.process_group_manager = None
+        dist.destroy_process_group()
