@@ -6,7 +6,7 @@
 // (the eager oracle LlamaRMSNorm, ref picotron/model.py:80-85, rounds x_hat to bf16 before
 // multiplying by w; the difference is within one bf16 ulp and covered by the parity tolerance).
 //
-// Layout: one wave64 per row, 4 rows per 256-thread workgroup; a lane owns 8 contiguous bf16
+// Layout (fwd): one wave64 per row, 4 rows per 256-thread workgroup; a lane owns 8 contiguous bf16
 // per 512-column chunk (16-byte loads), and keeps the whole row in registers (MAXC chunks) so x
 // is read from HBM exactly once. Algorithmic bytes: fwd 2*cols*2 B + 4 B per row,
 // bwd 3*cols*2 B + 4 B per row (+ the small fp32 dw partials).
@@ -80,70 +80,103 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd_kernel(const bf16_t* __restri
 
 // Backward: dx = rstd * (g - xhat * mean(g * xhat)), g = dy * w, xhat = x * rstd;
 // dw partial per workgroup (deterministic two-stage reduction, no atomics).
-template <int MAXC>
-__global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ dres,
-                                                          const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
-                                                          const float* __restrict__ rstd, bf16_t* __restrict__ dx,
-                                                          float* __restrict__ dw_part, int64_t rows, int cols) {
-  __shared__ float red[WAVES][MAXC * 512];
+// FULL: cols == MAXC * 512 (every lane chunk in range: no per-chunk predicates, which otherwise
+// make hipcc spill). NW waves per workgroup (16 up to 1024 columns, 8 up to 2048, 4 above — the
+// most that fit without spilling), one row per wave per pass, at most one workgroup per CU; the
+// per-wave dw partials accumulate in LDS and the workgroup's sum is one fp32 row per CU.
+template <int MAXC, int NW, bool FULL, bool RES>
+__global__ __launch_bounds__(NW * 64) void rmsnorm_bwd_kernel(const bf16_t* __restrict__ dy,
+                                                              const bf16_t* __restrict__ dres,
+                                                              const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
+                                                              const float* __restrict__ rstd, bf16_t* __restrict__ dx,
+                                                              float* __restrict__ dw_part, int64_t rows, int cols) {
+  __shared__ float red[NW * MAXC * 512];  // per-wave dw partial rows (accumulated in LDS, not registers)
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
-  float wf[MAXC][8], dwacc[MAXC][8];
+  float* myred = red + wid * MAXC * 512 + lane * 8;  // chunk c at + 512 c
 #pragma unroll
   for (int c = 0; c < MAXC; ++c) {
-    const int col = (c * 64 + lane) * 8;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) dwacc[c][j] = 0.f;
-    if (col < cols) load8(w + col, wf[c]);
+    *reinterpret_cast<f32x4*>(myred + 512 * c) = (f32x4)0.f;
+    *reinterpret_cast<f32x4*>(myred + 512 * c + 4) = (f32x4)0.f;
   }
-  for (int64_t row = (int64_t)blockIdx.x * WAVES + wid; row < rows; row += (int64_t)gridDim.x * WAVES) {
+  const bf16_t* wl = w + lane * 8;
+#pragma unroll 1
+  for (int64_t row = (int64_t)blockIdx.x * NW + wid; row < rows; row += (int64_t)gridDim.x * NW) {
     const float rs = rstd[row];
-    float xh[MAXC][8], g[MAXC][8];
+    const int64_t ro = row * cols + lane * 8;  // this lane's first element of the row; chunk c at + 512 c
+    const bf16_t* xr = x + ro;
+    const bf16_t* dr = dy + ro;
+    const bf16_t* rr = RES ? dres + ro : nullptr;
+    u16x8 xv[MAXC], dv[MAXC], rv[MAXC], wv[MAXC];
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {  // every load of the row in flight before any use (w: L1/L2 hits)
+      if (FULL || (c * 64 + lane) * 8 < cols) {
+        xv[c] = *reinterpret_cast<const u16x8*>(xr + 512 * c);
+        dv[c] = *reinterpret_cast<const u16x8*>(dr + 512 * c);
+        if constexpr (RES) rv[c] = *reinterpret_cast<const u16x8*>(rr + 512 * c);
+        wv[c] = *reinterpret_cast<const u16x8*>(wl + 512 * c);
+      }
+    }
     float dot = 0.f;
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) {
-      const int col = (c * 64 + lane) * 8;
-      if (col < cols) {
-        float d[8];
-        load8(x + row * cols + col, xh[c]);
-        load8(dy + row * cols + col, d);
+      if (FULL || (c * 64 + lane) * 8 < cols) {
+        f32x4 a = *reinterpret_cast<const f32x4*>(myred + 512 * c);
+        f32x4 bq = *reinterpret_cast<const f32x4*>(myred + 512 * c + 4);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          xh[c][j] *= rs;
-          g[c][j] = d[j] * wf[c][j];
-          dwacc[c][j] += d[j] * xh[c][j];
-          dot += g[c][j] * xh[c][j];
+          const float xh = bf2f(xv[c][j]) * rs, d = bf2f(dv[c][j]);
+          if (j < 4) a[j] += d * xh;
+          else bq[j - 4] += d * xh;
+          dot += d * bf2f(wv[c][j]) * xh;
         }
+        *reinterpret_cast<f32x4*>(myred + 512 * c) = a;
+        *reinterpret_cast<f32x4*>(myred + 512 * c + 4) = bq;
       }
     }
     dot = wave_sum(dot) / (float)cols;
+    bf16_t* dxr = dx + ro;
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) {
-      const int col = (c * 64 + lane) * 8;
-      if (col < cols) {
-        float o[8];
+      if (FULL || (c * 64 + lane) * 8 < cols) {
+        u16x8 o;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = rs * (g[c][j] - xh[c][j] * dot);
-        if (dres) {
-          float r[8];
-          load8(dres + row * cols + col, r);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) o[j] += r[j];
+        for (int j = 0; j < 8; ++j) {
+          const float xh = bf2f(xv[c][j]) * rs;
+          float v = rs * (bf2f(dv[c][j]) * bf2f(wv[c][j]) - xh * dot);
+          if constexpr (RES) v += bf2f(rv[c][j]);
+          o[j] = f2bf(v);
         }
-        store8(dx + row * cols + col, o);
+        *reinterpret_cast<u16x8*>(dxr + 512 * c) = o;
       }
     }
   }
-  // reduce the 4 waves' dw partials through LDS, write one fp32 row per workgroup
-#pragma unroll
-  for (int c = 0; c < MAXC; ++c)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) red[wid][(c * 64 + lane) * 8 + j] = dwacc[c][j];
+  // reduce the NW waves' dw partials (fixed order), one fp32 row per workgroup
   __syncthreads();
-  for (int col = threadIdx.x; col < cols; col += 256) {
-    float s = red[0][col] + red[1][col] + red[2][col] + red[3][col];
+  for (int col = threadIdx.x; col < cols; col += NW * 64) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < NW; ++k) s += red[k * MAXC * 512 + col];
     dw_part[(int64_t)blockIdx.x * cols + col] = s;
   }
+}
+
+template <int M>
+int launch_rmsnorm_bwd(const void* dy, const void* dres, const void* x, const void* w, const float* rstd, void* dx,
+                       float* part, int64_t rows, int c, int nb, hipStream_t s) {
+  constexpr int NW = M <= 2 ? 16 : (M == 4 ? 8 : 4);
+  auto go = [&](auto full, auto res) {
+    PICO_LAUNCH(PICO_K_RMSNORM_BWD, "rmsnorm_bwd", s,
+                (rmsnorm_bwd_kernel<M, NW, decltype(full)::value, decltype(res)::value><<<nb, NW * 64, 0, s>>>(
+                    (const bf16_t*)dy, (const bf16_t*)dres, (const bf16_t*)x, (const bf16_t*)w, rstd, (bf16_t*)dx,
+                    part, rows, c)));
+    return 0;
+  };
+  const bool full = c == M * 512;
+  if (full && dres) return go(std::true_type{}, std::true_type{});
+  if (full) return go(std::true_type{}, std::false_type{});
+  if (dres) return go(std::false_type{}, std::true_type{});
+  return go(std::false_type{}, std::false_type{});
 }
 
 // dw[col] = sum over the workgroup partials, in a fixed order (deterministic): a 256-thread
@@ -179,8 +212,11 @@ int maxc_for(int64_t cols) {
   return -1;
 }
 
-int bwd_blocks(int64_t rows) {  // one workgroup per CU at most: fewer dw partial rows to reduce
-  int64_t nb = (rows + WAVES - 1) / WAVES;
+constexpr int bwd_waves(int maxc) { return maxc <= 2 ? 16 : (maxc == 4 ? 8 : 4); }
+
+int bwd_blocks(int64_t rows, int64_t cols) {  // one workgroup per CU at most: few dw partial rows
+  const int nw = bwd_waves(maxc_for(cols));
+  int64_t nb = (rows + nw - 1) / nw;
   return (int)(nb < 256 ? nb : 256);
 }
 
@@ -216,7 +252,8 @@ int pico_rmsnorm_fwd(const void* x, const void* residual, const void* weight, vo
 }
 
 int64_t pico_rmsnorm_bwd_workspace_bytes(int64_t rows, int64_t cols) {
-  return (int64_t)bwd_blocks(rows) * cols * (int64_t)sizeof(float);
+  if (maxc_for(cols) <= 0) return 0;
+  return (int64_t)bwd_blocks(rows, cols) * cols * (int64_t)sizeof(float);
 }
 
 int pico_rmsnorm_bwd(const void* dy, const void* dresidual, const void* x, const void* weight, const float* rstd,
@@ -227,20 +264,18 @@ int pico_rmsnorm_bwd(const void* dy, const void* dresidual, const void* x, const
   const int mc = maxc_for(cols);
   PICO_REQUIRE(mc > 0 && mc <= 8, "pico_rmsnorm_bwd: cols=%lld > 4096 unsupported", (long long)cols);
   hipStream_t s = (hipStream_t)stream;
-  const int nb = bwd_blocks(rows);
+  const int nb = bwd_blocks(rows, cols);
   auto part = (float*)workspace;
   const int c = (int)cols;
-#define BWD_CASE(M)                                                                                          \
-  case M:                                                                                                    \
-    PICO_LAUNCH(PICO_K_RMSNORM_BWD, "rmsnorm_bwd", s,                                                        \
-                rmsnorm_bwd_kernel<M><<<nb, 256, 0, s>>>((const bf16_t*)dy, (const bf16_t*)dresidual,       \
-                                                         (const bf16_t*)x, (const bf16_t*)weight, rstd,      \
-                                                         (bf16_t*)dx, part, rows, c));                      \
-    break;
+  int rc = 0;
   switch (mc) {
-    BWD_CASE(1) BWD_CASE(2) BWD_CASE(4) BWD_CASE(8)
+    case 1: rc = launch_rmsnorm_bwd<1>(dy, dresidual, x, weight, rstd, dx, part, rows, c, nb, s); break;
+    case 2: rc = launch_rmsnorm_bwd<2>(dy, dresidual, x, weight, rstd, dx, part, rows, c, nb, s); break;
+    case 4: rc = launch_rmsnorm_bwd<4>(dy, dresidual, x, weight, rstd, dx, part, rows, c, nb, s); break;
+    case 8: rc = launch_rmsnorm_bwd<8>(dy, dresidual, x, weight, rstd, dx, part, rows, c, nb, s); break;
   }
-#undef BWD_CASE
+  if (rc) return rc;
+
   PICO_LAUNCH(PICO_K_RMSNORM_DW, "rmsnorm_dw", s,
               rmsnorm_dw_kernel<<<pico_cdiv(cols, 32), 256, 0, s>>>(part, (bf16_t*)dweight, nb, c));
   return 0;

@@ -1,0 +1,73 @@
+"""HBM-bound kernel micro-benchmark at the SmolLM-1.7B micro-batch shapes (T = 4 x 1024 tokens,
+hidden 2048, intermediate 8192, 32 + 32 heads of 64): RMSNorm fwd/bwd (residual form), RoPE (q|k in
+place on the fused qkv buffer), SwiGLU fwd/bwd (strided halves of the gate|up buffer), embedding
+bwd. Times each launch with the library's HIP-event timer; prints one JSON line per kernel with
+algorithmic GB/s (every input read once + every output written once)."""
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main(iters=50):
+    from picotron_amd import _lib as L
+    from picotron_amd import ops
+    L.load()
+    T, H, I, NH, D, V = 4096, 2048, 8192, 32, 64, 49152
+    bf = torch.bfloat16
+    dev = "cuda"
+    torch.manual_seed(0)
+    x = torch.randn(T, H, dtype=bf, device=dev, requires_grad=True)
+    r = torch.randn(T, H, dtype=bf, device=dev, requires_grad=True)
+    w = torch.ones(H, dtype=bf, device=dev, requires_grad=True)
+    qkv = torch.randn(4, 1024, 3 * NH, D, dtype=bf, device=dev)
+    cos = torch.randn(1024, D // 2, dtype=bf, device=dev)
+    sin = torch.randn(1024, D // 2, dtype=bf, device=dev)
+    gu = torch.randn(T, 2 * I, dtype=bf, device=dev)
+    h = torch.empty(T, I, dtype=bf, device=dev)
+    dh = torch.randn(T, I, dtype=bf, device=dev)
+    dgu = torch.empty_like(gu)
+    ids = torch.randint(0, V, (4, 1024), device=dev)
+    dy_emb = torch.randn(4, 1024, H, dtype=bf, device=dev)
+    gemb = torch.zeros(V, H, dtype=bf, device=dev)
+
+    def run_norm():
+        y, res = ops.rms_norm(x, w, 1e-5, residual=r, prenorm=True)
+        torch.autograd.backward([y, res], [torch.ones_like(y), torch.ones_like(res)])
+
+    cases = [
+        ("rmsnorm", run_norm, [L.K_RMSNORM_FWD, L.K_RMSNORM_BWD, L.K_RMSNORM_DW]),
+        ("rope", lambda: ops._rope_launch(qkv[:, :, :2 * NH], qkv[:, :, :2 * NH], cos, sin, False), [L.K_ROPE]),
+        ("swiglu", lambda: (ops._swiglu_fwd(gu, gu[:, I:], h, T, I, 2 * I, I),
+                            ops._swiglu_bwd(dh, gu, gu[:, I:], dgu, dgu[:, I:], T, I, 2 * I, I)),
+         [L.K_SWIGLU_FWD, L.K_SWIGLU_BWD]),
+        ("embedding", lambda: ops._embedding_bwd_into(gemb, ids, dy_emb, 1.0), [L.K_EMBEDDING_BWD]),
+    ]
+    work = {L.K_RMSNORM_FWD: 4 * T * H * 2 + 4 * T, L.K_RMSNORM_BWD: 4 * T * H * 2 + 4 * T,
+            L.K_ROPE: 2 * T * 2 * NH * D * 2, L.K_SWIGLU_FWD: 3 * T * I * 2, L.K_SWIGLU_BWD: 5 * T * I * 2,
+            L.K_EMBEDDING_BWD: T * H * 2 + 2 * T * H * 2}
+    for name, fn, kids in cases:
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        for k in kids:
+            L.prof_enable(k, iters + 8)
+        for _ in range(iters):
+            fn()
+        torch.cuda.synchronize()
+        for k in kids:
+            ms, n = L.prof_collect(k)
+            us = 1e3 * ms / max(n, 1)
+            out = {"kernel": L.KERNEL_NAMES[k], "avg_us": round(us, 2), "launches": n}
+            if k in work:
+                out["GB_s"] = round(work[k] / (us * 1e-6) / 1e9, 1)
+                out["frac_of_8TBs"] = round(out["GB_s"] / 8000, 3)
+            print(json.dumps(out), flush=True)
+        L.load().pico_prof_enable(0, 0)
+
+
+if __name__ == "__main__":
+    main()
