@@ -21,6 +21,8 @@
  *                                                                      (ref picotron/data_parallel/bucket.py:30)
  *   pico_cast_f32_bf16        <- p.grad = p.main_grad.to(p.dtype)    (ref picotron/data_parallel/data_parallel.py:165)
  *   pico_scale_f32            <- grad_data /= process_group_size     (ref picotron/data_parallel/bucket.py:30)
+ *   pico_cross_entropy_fwd/_bwd <- F.cross_entropy(logits, target, reduction='mean')
+ *                                 (ref train.py:46-49, picotron/pipeline_parallel/pipeline_parallel.py:68,98)
  *   pico_embedding_bwd        <- backward of F.embedding (ref picotron/model.py:223-224) + the micro-batch
  *                                 gradient accumulation (data_parallel.py:131 / autograd's grad += dW)
  *
@@ -59,7 +61,9 @@ enum {
   PICO_K_SCALE = 13,
   PICO_K_ATTN_MERGE = 14,
   PICO_K_EMBEDDING_BWD = 15,
-  PICO_K_COUNT = 16
+  PICO_K_CE_FWD = 16,
+  PICO_K_CE_BWD = 17,
+  PICO_K_COUNT = 18
 };
 
 int pico_abi_version(void);
@@ -157,6 +161,18 @@ int pico_cast_f32_bf16(const float* src, void* dst, int64_t n, void* stream);
  * for every id present: grad[id] = (grad[id] + sum of its dy rows in position order) * scale. */
 int pico_embedding_bwd(const int64_t* sorted_ids, const int64_t* sorted_pos, const void* dy, void* grad,
                        int64_t n_tokens, int64_t dim, int grad_is_f32, float scale, void* stream);
+
+/* ---- softmax cross-entropy (mean over non-ignored rows) ----
+ * logits: [rows, vocab] bf16, row stride ld (elements); target: [rows] int64.
+ * fwd: lse[i] = log sum_j exp(logits[i][j]) (fp32), loss[i] = lse[i] - logits[i][target[i]] (0 for
+ *      target == ignore_index). The caller sums loss[] and divides by the non-ignored count.
+ * bwd: dlogits[i][j] = (exp(logits[i][j] - lse[i]) - [j == target[i]]) * (*grad_scale) (0 rows for
+ *      ignored targets); grad_scale is a DEVICE fp32 scalar (grad_out / n_valid), row stride ldd. */
+int pico_cross_entropy_fwd(const void* logits, int64_t ld, const int64_t* target, float* lse, float* loss,
+                           int64_t rows, int64_t vocab, int64_t ignore_index, void* stream);
+int pico_cross_entropy_bwd(const void* logits, int64_t ld, const int64_t* target, const float* lse,
+                           const float* grad_scale, void* dlogits, int64_t ldd, int64_t rows, int64_t vocab,
+                           int64_t ignore_index, void* stream);
 
 #ifdef __cplusplus
 }

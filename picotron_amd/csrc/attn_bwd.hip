@@ -25,6 +25,12 @@
 // FLOPs per (b, h): 10 * Sq * Sk * D (halved by the causal mask); 2.5x the forward.
 #include "attn_common.h"
 
+// Build-time variants (A/B measurement only; the shipped defaults are the measured-best):
+//   PICO_BWD_DQ_UNROLL: dQ key steps fully unrolled + predicated (1) or a runtime-bounded loop (0)
+#ifndef PICO_BWD_DQ_UNROLL
+#define PICO_BWD_DQ_UNROLL 0
+#endif
+
 namespace {
 
 constexpr int BK = 256;  // keys per workgroup
@@ -46,6 +52,23 @@ struct BwdCfg {
   static constexpr int NP = 2 * NQP + 1;        // pieces per tile
   static constexpr int NPW = (NP + 7) / 8;      // max pieces per wave
 };
+
+// s_waitcnt vmcnt(n) for a wave-uniform runtime n (the immediate must be a constant)
+PICO_DEV void wait_vmcnt(int n) {
+  switch (n) {
+#define PICO_VMCNT_CASE(N) \
+  case N:                  \
+    asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); \
+    break;
+    PICO_VMCNT_CASE(1) PICO_VMCNT_CASE(2) PICO_VMCNT_CASE(3) PICO_VMCNT_CASE(4) PICO_VMCNT_CASE(5)
+    PICO_VMCNT_CASE(6) PICO_VMCNT_CASE(7) PICO_VMCNT_CASE(8) PICO_VMCNT_CASE(9) PICO_VMCNT_CASE(10)
+    PICO_VMCNT_CASE(11) PICO_VMCNT_CASE(12) PICO_VMCNT_CASE(13) PICO_VMCNT_CASE(14) PICO_VMCNT_CASE(15)
+    PICO_VMCNT_CASE(16) PICO_VMCNT_CASE(17) PICO_VMCNT_CASE(18) PICO_VMCNT_CASE(19) PICO_VMCNT_CASE(20)
+#undef PICO_VMCNT_CASE
+    default:
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+}
 
 // XOR applied to the 16-B chunk index of image row `row` (see lds_off in attn_common.h)
 template <int D>
@@ -104,7 +127,8 @@ constexpr int bwd_waves_per_eu() { return D == 64 ? 2 : 1; }
 template <int D, bool CAUSAL>
 __global__ __launch_bounds__(512, bwd_waves_per_eu<D>()) void attn_bwd_kernel(
     const pico_attn_args a, float scale, float scale_log2, const float* __restrict__ delta_g,
-    const float* __restrict__ lse2_g, int sq_pad, float* __restrict__ dq_part, int64_t slab) {
+    const float* __restrict__ lse2_g, int sq_pad, float* __restrict__ dq_part, int64_t slab,
+    float* __restrict__ trash) {
   using C = BwdCfg<D>;
   constexpr int KS = C::KS, DT = C::DT, CPR = C::CPR;
   __shared__ __attribute__((aligned(16))) char smem[C::SMEM];
@@ -227,24 +251,33 @@ __global__ __launch_bounds__(512, bwd_waves_per_eu<D>()) void attn_bwd_kernel(
       const int tl = wave + 8 * tt;
       const int qi = tl / (D / 16), di = tl % (D / 16);
       f32x4 acc = (f32x4)0.f;
+      // all BK/32 key steps unrolled so the transposed LDS reads issue back to back; steps past
+      // kmax read (stale) LDS and are zeroed in the A operand instead of branched around
+#if PICO_BWD_DQ_UNROLL
+#pragma unroll
+      for (int kk = 0; kk < BK; kk += 32) {
+#else
       for (int kk = 0; kk < kmax; kk += 32) {
-        {
-          // A = dS[q = 16 qi + (lane & 15)][key = kk + 8 g16 + j]: transposed read of the [key][q] image
-          const int row = kk + 8 * g16 + (i16 >> 2);
-          const int qc = 16 * qi + 4 * (i16 & 3);
-          const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(dsimg + ds_img_off(row, qc)));
-          const i16x4 up = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(dsimg + ds_img_off(row + 4, qc)));
-          typedef __attribute__((ext_vector_type(8))) short i16x8;
-          const i16x8 av = {lo[0], lo[1], lo[2], lo[3], up[0], up[1], up[2], up[3]};
-          const bf16x8 bf = lds_read_tr16<D>(kimg, kk, di * 16, lane);
-          acc = mfma16(__builtin_bit_cast(bf16x8, av), bf, acc);
-        }
+#endif
+        // A = dS[q = 16 qi + (lane & 15)][key = kk + 8 g16 + j]: transposed read of the [key][q] image
+        const int row = kk + 8 * g16 + (i16 >> 2);
+        const int qc = 16 * qi + 4 * (i16 & 3);
+        const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(dsimg + ds_img_off(row, qc)));
+        const i16x4 up = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(dsimg + ds_img_off(row + 4, qc)));
+        typedef __attribute__((ext_vector_type(8))) short i16x8;
+        i16x8 av = {lo[0], lo[1], lo[2], lo[3], up[0], up[1], up[2], up[3]};
+        if (PICO_BWD_DQ_UNROLL && kk >= kmax) av = (i16x8)0;
+        const bf16x8 bf = lds_read_tr16<D>(kimg, kk, di * 16, lane);
+        acc = mfma16(__builtin_bit_cast(bf16x8, av), bf, acc);
       }
+      // every lane stores (rows past Sq go to a trash slot), so the per-tile count of vector-memory
+      // instructions is fixed and the ring's vmcnt waits stay exact
       float* dst = dq_part + kb * slab + (int64_t)b * Sq * Hq * D + hq * D + di * 16 + i16;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int q = q0 + qi * 16 + 4 * g16 + j;
-        if (q < Sq) dst[(int64_t)q * Hq * D] = acc[j] * scale;
+        float* p = q < Sq ? dst + (int64_t)q * Hq * D : trash + lane;
+        *p = acc[j] * scale;
       }
     }
   };
@@ -252,16 +285,15 @@ __global__ __launch_bounds__(512, bwd_waves_per_eu<D>()) void attn_bwd_kernel(
   for (int t = 0; t < ntiles; ++t) {
     // this wave's pieces of tile t landed (tile t+1's stay in flight), then everyone's (barrier);
     // the barrier also retires every read of iteration t-1 (ring slot (t+2) % 3, dS image)
-    if (t + 1 < ntiles) {
-      if (my_np == C::NPW) {
-        if constexpr (C::NPW == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-      } else {
-        if constexpr (C::NPW == 2) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-      }
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    {
+      // vector-memory ops this wave issued after tile t's DMA pieces: dQ stores of tile t-2, the
+      // pieces of tile t+1, dQ stores of tile t-1 (issue order) — they may stay in flight
+      constexpr int NST = 4 * ((BQ / 16) * (D / 16) / 8);
+      int younger = 0;
+      if (t >= 2) younger += NST;
+      if (t + 1 < ntiles) younger += my_np;
+      if (t >= 1) younger += NST;
+      wait_vmcnt(younger);
     }
     __syncthreads();
     if (t + 2 < ntiles) issue(t + 2);
@@ -409,6 +441,7 @@ int launch_bwd(const pico_attn_args* a, hipStream_t s) {
   float* lse2 = (float*)a->workspace;
   float* delta = lse2 + lsd_floats(a);
   float* dq_part = delta + lsd_floats(a);
+  float* trash = dq_part + (int64_t)((a->seqlen_k + BK - 1) / BK) * a->batch * a->seqlen_q * a->heads_q * D;
   const int64_t slab = a->batch * a->seqlen_q * a->heads_q * D;
   const int64_t rows = a->batch * a->seqlen_q * a->heads_q;
   const int row_blocks = pico_cdiv(rows * (D / 8), 256);
@@ -422,11 +455,11 @@ int launch_bwd(const pico_attn_args* a, hipStream_t s) {
     if (a->causal) {
       PICO_LAUNCH(PICO_K_ATTN_BWD, "attn_bwd", s,
                   attn_bwd_kernel<D, true><<<(int)nblk, 512, 0, s>>>(*a, a->softmax_scale, sl2, delta, lse2, sq_pad,
-                                                                     dq_part, slab));
+                                                                     dq_part, slab, trash));
     } else {
       PICO_LAUNCH(PICO_K_ATTN_BWD, "attn_bwd", s,
                   attn_bwd_kernel<D, false><<<(int)nblk, 512, 0, s>>>(*a, a->softmax_scale, sl2, delta, lse2, sq_pad,
-                                                                      dq_part, slab));
+                                                                      dq_part, slab, trash));
     }
   }
   if (a->causal) {
@@ -468,7 +501,8 @@ int64_t pico_attn_args_size(void) { return (int64_t)sizeof(pico_attn_args); }
 int64_t pico_attn_bwd_workspace_bytes(const pico_attn_args* a) {
   // lse2, delta [B*Hq*Sq_pad] fp32 + one fp32 dQ partial slab [B, Sq, Hq, D] per 256-key block
   const int64_t nkb = (a->seqlen_k + BK - 1) / BK;
-  return (2 * lsd_floats(a) + nkb * a->batch * a->seqlen_q * a->heads_q * a->head_dim) * 4;
+  // + 64 floats of trash for the dQ stores of padded query rows
+  return (2 * lsd_floats(a) + nkb * a->batch * a->seqlen_q * a->heads_q * a->head_dim + 64) * 4;
 }
 
 int pico_attn_bwd(const pico_attn_args* a, void* stream) {

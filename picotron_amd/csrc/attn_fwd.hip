@@ -26,6 +26,20 @@
 
 #include "attn_common.h"
 
+// Build-time variants (A/B measurement only; the shipped defaults are the measured-best):
+//   PICO_FWD_RESCALE_THR: rescale O only when a row max grows by more than THR (log2 units; 0 =
+//     rescale on every growth). > 0 (cdna_hip_programming.md T13) lets P reach 2^THR: l and O stay
+//     exact in fp32 and P is bf16-rounded with the same relative precision as any P <= 1; the final
+//     1/l normalisation is unchanged. Measured: THR = 8 -2.7 % (D=64) / -4 % (D=128) kernel time.
+//   PICO_FWD_EARLY_V: issue the V^T transposed reads before the softmax VALU (1), after it (0), or
+//     by head_dim (-1: early for D = 128 only, where it measured -2.5 %; neutral at D = 64).
+#ifndef PICO_FWD_RESCALE_THR
+#define PICO_FWD_RESCALE_THR 8
+#endif
+#ifndef PICO_FWD_EARLY_V
+#define PICO_FWD_EARLY_V -1
+#endif
+
 namespace {
 
 constexpr int BM = 128;  // query rows per workgroup (32 per wave)
@@ -70,6 +84,7 @@ PICO_DEV float halves_sum(float x) {
 template <int D, bool CAUSAL>
 __global__ __launch_bounds__(256, FwdCfg<D>::WAVES_PER_EU) void attn_fwd_kernel(const pico_attn_args a, float scale_log2) {
   using C = FwdCfg<D>;
+  constexpr bool EARLY_V = PICO_FWD_EARLY_V < 0 ? D == 128 : PICO_FWD_EARLY_V != 0;
   constexpr int KS = C::KS;  // k-steps of the S^T product
   constexpr int DT = C::DT;  // 32-wide output tiles of O^T
   __shared__ __attribute__((aligned(16))) char smem[C::NBUF * C::SLOT];
@@ -176,10 +191,9 @@ __global__ __launch_bounds__(256, FwdCfg<D>::WAVES_PER_EU) void attn_fwd_kernel(
   float m_i = -INFINITY;  // running max of scale*log2e*s (scaled domain)
   float l_i = 0.f;        // per-lane partial row sum (this lane's keys only)
 
-  // P^T (keys 32 kt .. 32 kt + 31 of the tile) times V: 2 * DT MFMAs.
-  auto pv_half_impl = [&](const f32x16& p, unsigned va, auto kt_tag) __attribute__((always_inline)) {
+  // V^T operands for keys 32 kt .. 32 kt + 31 of the tile (2 st x DT, inline-asm transposed reads)
+  auto v_reads = [&](bf16x8 (&vf)[2][DT], unsigned va, auto kt_tag) __attribute__((always_inline)) {
     constexpr int KT = decltype(kt_tag)::value;
-    bf16x8 vf[2][DT];
     static_for<2>([&](auto st_) {
       constexpr int ST = decltype(st_)::value;
       static_for<DT>([&](auto dt_) {
@@ -187,6 +201,9 @@ __global__ __launch_bounds__(256, FwdCfg<D>::WAVES_PER_EU) void attn_fwd_kernel(
         vf[ST][DTI] = tr_operand_imm<BN * D * 2 + DTI * C::VIMG + (32 * KT + 16 * ST) * 64, 8 * 64>(va);
       });
     });
+  };
+  // P^T (keys 32 kt .. 32 kt + 31 of the tile) times V: 2 * DT MFMAs.
+  auto pv_mfma = [&](const f32x16& p, const bf16x8 (&vf)[2][DT]) __attribute__((always_inline)) {
     float pv[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) pv[j] = p[j];
@@ -210,6 +227,11 @@ __global__ __launch_bounds__(256, FwdCfg<D>::WAVES_PER_EU) void attn_fwd_kernel(
         s[kt] = mfma32(kf, qf[ks], s[kt]);
       }
     }
+    bf16x8 vf0[2][DT], vf1[2][DT];
+    if constexpr (EARLY_V) {  // in flight during the softmax VALU below
+      v_reads(vf0, vaddr, std::integral_constant<int, 0>{});
+      v_reads(vf1, vaddr, std::integral_constant<int, 1>{});
+    }
     // lane holds row my_q, keys n0 + 32 kt + acc_row(i, h) = n0 + 4h + c(kt, i)
     if (mask) {  // wave-uniform
       const int rel = lim_lane - n0 - 4 * h;  // key allowed iff c <= rel
@@ -228,7 +250,7 @@ __global__ __launch_bounds__(256, FwdCfg<D>::WAVES_PER_EU) void attn_fwd_kernel(
       for (int i = (kt == 0 ? 1 : 0); i < 16; ++i) mx = fmaxf(mx, s[kt][i]);
     const float m_tile = halves_max(mx) * scale_log2;
     // rescale only when some row's max grew (wave-uniform); exact
-    if (__builtin_amdgcn_ballot_w64(m_tile > m_i)) {
+    if (__builtin_amdgcn_ballot_w64(m_tile > m_i + (float)PICO_FWD_RESCALE_THR)) {
       const float m_new = fmaxf(m_i, m_tile);
       const float alpha = m_i == -INFINITY ? 0.f : fast_exp2(m_i - m_new);
       l_i *= alpha;
@@ -252,8 +274,15 @@ __global__ __launch_bounds__(256, FwdCfg<D>::WAVES_PER_EU) void attn_fwd_kernel(
     l_i += lsum0 + lsum1;
     // O^T[dt] += V^T * P^T : A = V^T via transposed LDS reads (per kt: 2 st x DT operands, issued
     // together, one wait), B = packed P^T registers
-    pv_half_impl(s[0], vaddr, std::integral_constant<int, 0>{});
-    pv_half_impl(s[1], vaddr, std::integral_constant<int, 1>{});
+    if constexpr (!EARLY_V) {
+      v_reads(vf0, vaddr, std::integral_constant<int, 0>{});
+      pv_mfma(s[0], vf0);
+      v_reads(vf1, vaddr, std::integral_constant<int, 1>{});
+      pv_mfma(s[1], vf1);
+    } else {
+      pv_mfma(s[0], vf0);
+      pv_mfma(s[1], vf1);
+    }
   };
 
   constexpr int P = C::NBUF - 1;  // prefetch distance

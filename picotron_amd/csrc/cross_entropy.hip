@@ -1,0 +1,154 @@
+// Fused softmax cross-entropy over the LM-head logits for gfx950 (HBM-bound).
+//
+// Replaces F.cross_entropy(logits, target, reduction='mean') (ref train.py:46-49,
+// picotron/pipeline_parallel/pipeline_parallel.py:68,98). ATen runs it as log_softmax -> nll_loss
+// and back (nll_loss backward materialises a dense one-hot gradient, log_softmax backward re-reads
+// it and the saved log-probabilities): about six sweeps over the [tokens, vocab] logits (SmolLM:
+// 4096 x 49152 bf16 = 403 MB each). Here:
+//   fwd: one read of the logits -> per-row lse (fp32) and loss_i = lse_i - x_i[t_i];
+//   bwd: one read of the logits -> dlogits = (exp(x - lse) - onehot(t)) * grad_out / n_valid, written
+//        once (bf16), with grad_out / n_valid read from device memory (no host sync).
+// Rows whose target == ignore_index contribute neither loss nor gradient (torch semantics).
+// One 256-thread workgroup per row; a thread keeps its NCH 16-byte chunks of the row in registers
+// between the max and the sum-of-exp passes, so each pass reads the row from HBM once.
+// fp32 math throughout (torch: fp32 opmath inside log_softmax, bf16 log-probs in between).
+#include "common.h"
+
+namespace {
+
+PICO_DEV float block_reduce(float v, float* red, bool is_max) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const float u = __shfl_xor(v, o, 64);
+    v = is_max ? fmaxf(v, u) : v + u;
+  }
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  __syncthreads();
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  float r = red[0];
+#pragma unroll
+  for (int k = 1; k < 4; ++k) r = is_max ? fmaxf(r, red[k]) : r + red[k];
+  return r;
+}
+
+template <int NCH>
+__global__ __launch_bounds__(256) void ce_fwd_kernel(const bf16_t* __restrict__ logits, int64_t ld,
+                                                     const int64_t* __restrict__ target, float* __restrict__ lse,
+                                                     float* __restrict__ loss, int vocab, int64_t ignore) {
+  __shared__ float red[4];
+  const int64_t row = blockIdx.x;
+  const bf16_t* x = logits + row * ld;
+  const int nchunk = vocab / 8;
+  u16x8 v[NCH];
+  float m = -INFINITY;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int ch = threadIdx.x + 256 * c;
+    if (ch < nchunk) {
+      v[c] = *reinterpret_cast<const u16x8*>(x + 8 * ch);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) m = fmaxf(m, bf2f(v[c][j]));
+    }
+  }
+  m = block_reduce(m, red, true);
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int ch = threadIdx.x + 256 * c;
+    if (ch < nchunk) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += __expf(bf2f(v[c][j]) - m);
+    }
+  }
+  s = block_reduce(s, red, false);
+  if (threadIdx.x == 0) {
+    const float l = m + __logf(s);
+    const int64_t t = target[row];
+    lse[row] = l;
+    loss[row] = (t == ignore || t < 0 || t >= vocab) ? 0.f : l - bf2f(x[t]);
+  }
+}
+
+template <int NCH>
+__global__ __launch_bounds__(256) void ce_bwd_kernel(const bf16_t* __restrict__ logits, int64_t ld,
+                                                     const int64_t* __restrict__ target, const float* __restrict__ lse,
+                                                     const float* __restrict__ gscale, bf16_t* __restrict__ dlogits,
+                                                     int64_t ldd, int vocab, int64_t ignore) {
+  const int64_t row = blockIdx.x;
+  const bf16_t* x = logits + row * ld;
+  bf16_t* dx = dlogits + row * ldd;
+  const int nchunk = vocab / 8;
+  const int64_t t = target[row];
+  const bool skip = t == ignore || t < 0 || t >= vocab;
+  const float g = skip ? 0.f : *gscale;
+  const float l = lse[row];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int ch = threadIdx.x + 256 * c;
+    if (ch < nchunk) {
+      const u16x8 xv = *reinterpret_cast<const u16x8*>(x + 8 * ch);
+      u16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float p = __expf(bf2f(xv[j]) - l);
+        if (8 * ch + j == t) p -= 1.f;
+        o[j] = f2bf(p * g);
+      }
+      *reinterpret_cast<u16x8*>(dx + 8 * ch) = o;
+    }
+  }
+}
+
+int nch_for(int64_t vocab) {
+  const int64_t per = (vocab / 8 + 255) / 256;
+  for (int n : {4, 8, 16, 24, 32, 48, 64})
+    if (per <= n) return n;
+  return -1;
+}
+
+}  // namespace
+
+#define CE_SWITCH(NCHV, CALL)                      \
+  switch (NCHV) {                                  \
+    case 4: { constexpr int N = 4; CALL; } break;   \
+    case 8: { constexpr int N = 8; CALL; } break;   \
+    case 16: { constexpr int N = 16; CALL; } break; \
+    case 24: { constexpr int N = 24; CALL; } break; \
+    case 32: { constexpr int N = 32; CALL; } break; \
+    case 48: { constexpr int N = 48; CALL; } break; \
+    case 64: { constexpr int N = 64; CALL; } break; \
+  }
+
+extern "C" int pico_cross_entropy_fwd(const void* logits, int64_t ld, const int64_t* target, float* lse, float* loss,
+                                      int64_t rows, int64_t vocab, int64_t ignore_index, void* stream) {
+  PICO_REQUIRE(rows >= 0 && vocab > 0 && vocab % 8 == 0 && ld % 8 == 0 && ld >= vocab,
+               "pico_cross_entropy_fwd: vocab (%lld) and row stride must be multiples of 8", (long long)vocab);
+  const int nch = nch_for(vocab);
+  PICO_REQUIRE(nch > 0, "pico_cross_entropy_fwd: vocab %lld too large", (long long)vocab);
+  PICO_REQUIRE(rows < (1ll << 31), "pico_cross_entropy_fwd: too many rows");
+  if (rows == 0) return 0;
+  PICO_REQUIRE(logits && target && lse && loss, "pico_cross_entropy_fwd: null pointer");
+  hipStream_t s = (hipStream_t)stream;
+  CE_SWITCH(nch, PICO_LAUNCH(PICO_K_CE_FWD, "cross_entropy_fwd", s,
+                             ce_fwd_kernel<N><<<(int)rows, 256, 0, s>>>((const bf16_t*)logits, ld, target, lse, loss,
+                                                                        (int)vocab, ignore_index)))
+  return 0;
+}
+
+extern "C" int pico_cross_entropy_bwd(const void* logits, int64_t ld, const int64_t* target, const float* lse,
+                                      const float* grad_scale, void* dlogits, int64_t ldd, int64_t rows, int64_t vocab,
+                                      int64_t ignore_index, void* stream) {
+  PICO_REQUIRE(rows >= 0 && vocab > 0 && vocab % 8 == 0 && ld % 8 == 0 && ldd % 8 == 0,
+               "pico_cross_entropy_bwd: vocab and row strides must be multiples of 8");
+  const int nch = nch_for(vocab);
+  PICO_REQUIRE(nch > 0, "pico_cross_entropy_bwd: vocab %lld too large", (long long)vocab);
+  if (rows == 0) return 0;
+  PICO_REQUIRE(logits && target && lse && grad_scale && dlogits, "pico_cross_entropy_bwd: null pointer");
+  hipStream_t s = (hipStream_t)stream;
+  CE_SWITCH(nch, PICO_LAUNCH(PICO_K_CE_BWD, "cross_entropy_bwd", s,
+                             ce_bwd_kernel<N><<<(int)rows, 256, 0, s>>>((const bf16_t*)logits, ld, target, lse,
+                                                                        grad_scale, (bf16_t*)dlogits, ldd, (int)vocab,
+                                                                        ignore_index)))
+  return 0;
+}

@@ -332,6 +332,54 @@ class _EmbeddingFn(torch.autograd.Function):
         return None, g
 
 
+class _CrossEntropyFn(torch.autograd.Function):
+    """F.cross_entropy(logits, target, reduction='mean') on pico_cross_entropy_fwd/_bwd: one read of
+    the logits forward, one read + one write backward (ref train.py:46-49). The loss is returned in
+    the logits' dtype, as ATen's is."""
+
+    @staticmethod
+    def forward(ctx, logits, target, ignore_index):
+        _need(logits, "logits")
+        rows, vocab = logits.shape
+        if logits.stride(1) != 1:
+            logits = logits.contiguous()
+        t = target.reshape(-1)
+        if t.dtype != torch.int64:
+            t = t.long()
+        t = t.contiguous()
+        lse = torch.empty(rows, dtype=torch.float32, device=logits.device)
+        loss_rows = torch.empty(rows, dtype=torch.float32, device=logits.device)
+        _lib.check(_lib.load().pico_cross_entropy_fwd(_lib.ptr(logits), logits.stride(0), _lib.ptr(t), _lib.ptr(lse),
+                                                      _lib.ptr(loss_rows), rows, vocab, int(ignore_index),
+                                                      _lib.stream_of(logits)), "pico_cross_entropy_fwd")
+        n_valid = (t != ignore_index).sum().to(torch.float32)  # device scalar, no host sync
+        loss = loss_rows.sum() / n_valid
+        ctx.save_for_backward(logits, t, lse, n_valid)
+        ctx.ignore_index = int(ignore_index)
+        return loss.to(logits.dtype)
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        logits, t, lse, n_valid = ctx.saved_tensors
+        rows, vocab = logits.shape
+        gscale = (grad_out.to(torch.float32) / n_valid).reshape(1).contiguous()
+        dlogits = torch.empty((rows, vocab), dtype=logits.dtype, device=logits.device)
+        _lib.check(_lib.load().pico_cross_entropy_bwd(_lib.ptr(logits), logits.stride(0), _lib.ptr(t), _lib.ptr(lse),
+                                                      _lib.ptr(gscale), _lib.ptr(dlogits), dlogits.stride(0), rows,
+                                                      vocab, ctx.ignore_index, _lib.stream_of(logits)),
+                   "pico_cross_entropy_bwd")
+        return dlogits, None, None
+
+
+def cross_entropy(logits, target, ignore_index=-100, reduction="mean"):
+    """F.cross_entropy for [N, V] bf16 logits on a HIP device (mean reduction)."""
+    if reduction != "mean":
+        raise NotImplementedError("picotron_amd.cross_entropy: only reduction='mean'")
+    if logits.dim() != 2:
+        raise ValueError("picotron_amd.cross_entropy: logits must be [N, V]")
+    return _CrossEntropyFn.apply(logits, target, ignore_index)
+
+
 def embedding(ids, w):
     if not wgrad_fusion_enabled():
         return torch.nn.functional.embedding(ids, w)

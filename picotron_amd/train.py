@@ -1,6 +1,7 @@
 """Training step and loop — semantics of the reference train.py (train_step :29-55, loop :219-259),
 on the gfx950 hot path. Data is synthetic (no network); the model is built by
 picotron_amd.model.build_llama with the reference's init (seed first)."""
+import os
 import time
 
 import torch
@@ -13,11 +14,20 @@ from . import process_group_manager as pgm
 MI355X_BF16_PEAK = 256 * 4096 * 2.4e9
 
 
+def _cross_entropy(outputs, targets):
+    """F.cross_entropy (ref train.py:46-49) on the fused HIP kernel for bf16 logits on the GPU."""
+    if outputs.is_cuda and outputs.dtype == torch.bfloat16 and outputs.shape[-1] % 8 == 0 and \
+            os.getenv("PICO_UNFUSED", "0") != "1":
+        from . import ops
+        return ops.cross_entropy(outputs, targets)
+    return F.cross_entropy(outputs, targets, reduction="mean")
+
+
 def _micro_batch(model, input_ids, target_ids, grad_acc_steps):
     outputs = model(input_ids=input_ids)
     batch_size, seq_len = input_ids.shape
     outputs = outputs.view(seq_len * batch_size, -1)
-    loss = F.cross_entropy(outputs, target_ids.reshape(-1), reduction="mean") / grad_acc_steps
+    loss = _cross_entropy(outputs, target_ids.reshape(-1)) / grad_acc_steps
     loss.backward()
     return loss.detach()
 

@@ -339,3 +339,35 @@ def test_embedding_bwd_matches_dense(grad_dtype):
     again = g0.clone()
     _embedding_bwd_into(again, ids, dy, scale)
     assert torch.equal(again, got)
+
+
+# ------------------------------------------------------------------------------------------ cross-entropy
+@pytest.mark.parametrize("V,ignore", [(49152, False), (512, True), (32000, False)])
+def test_cross_entropy_matches_torch(V, ignore):
+    """pico_cross_entropy_fwd/_bwd == F.cross_entropy(mean) on the same bf16 logits: loss within bf16
+    rounding of an fp64 reference, dlogits (incl. a non-unit upstream gradient) vs fp64 softmax - onehot,
+    ignored targets (-100) excluded from the mean and given zero gradient."""
+    from picotron_amd import ops
+    torch.manual_seed(V)
+    N = 300
+    logits = (torch.randn(N, V, device=DEV) * 3).to(BF).requires_grad_(True)
+    tgt = torch.randint(0, V, (N,), device=DEV)
+    if ignore:
+        tgt[::7] = -100
+    loss = ops.cross_entropy(logits, tgt)
+    (loss * 0.25).backward()
+    x = logits.detach().double()
+    keep = tgt != -100
+    lse = torch.logsumexp(x, dim=1)
+    ref_rows = lse - x.gather(1, tgt.clamp_min(0)[:, None]).squeeze(1)
+    ref = ref_rows[keep].mean()
+    assert loss.dtype == BF
+    assert abs(float(loss) - float(ref)) <= 8e-3 * abs(float(ref)) + 1e-3
+    p = torch.softmax(x, dim=1)
+    p[torch.arange(N, device=DEV), tgt.clamp_min(0)] -= 1
+    p[~keep] = 0
+    p *= 0.25 / keep.sum()
+    assert rel_l2(logits.grad.cpu(), p.cpu()) < 8e-3
+    assert float(logits.grad[~keep].abs().sum()) == 0.0
+    t_loss = torch.nn.functional.cross_entropy(logits.detach(), tgt)
+    assert abs(float(t_loss) - float(loss)) <= 1.6e-2 * abs(float(ref)) + 2e-3
