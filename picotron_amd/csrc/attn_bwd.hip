@@ -30,6 +30,11 @@
 #ifndef PICO_BWD_DQ_UNROLL
 #define PICO_BWD_DQ_UNROLL 0
 #endif
+//   PICO_BWD_WAVES_PER_EU_D64: register budget for D = 64 (2: <= 256 VGPRs, one 512-thread workgroup
+//     per CU; 4: <= 128 VGPRs, two per CU — their LDS (75 KiB each) fits)
+#ifndef PICO_BWD_WAVES_PER_EU_D64
+#define PICO_BWD_WAVES_PER_EU_D64 2
+#endif
 
 namespace {
 
@@ -78,10 +83,41 @@ PICO_DEV int swz(int row) {
   return y ^ ((y & 1) << 2);
 }
 
-// byte offset of q-pair column `q` (even) of key row `key` in the dS^T image: 64-B rows, the two
-// 32-B halves swapped on odd 8-row groups (conflict-free transposed reads over 8-row strides)
+// byte offset of column q of key row `key` in the dS^T image [key][q] (64-B rows of eight 8-B pieces,
+// piece index XOR (key >> 1) & 7): the 4 x ds_write_b64 per lane (16 consecutive keys, one piece) and
+// the transposed reads of the dQ A operand are both bank-conflict free (scripts/lds_conflicts.py;
+// the previous half-swap layout made the writes 4-way)
 PICO_DEV int ds_img_off(int key, int q) {
-  return key * 64 + ((((q >> 4) ^ (key >> 3)) & 1) << 5) + ((q & 15) << 1);
+  return key * 64 + 8 * ((q >> 2) ^ ((key >> 1) & 7)) + 2 * (q & 3);
+}
+
+// K block image [256 keys][D]: 16-B chunk index XOR a linear function of row bits 0-3, found by
+// exhaustive search (scripts/lds_conflicts.py) so that both uses are conflict free: the ds_read_b128
+// row reads of the S operand (rows 32w + r) and the ds_read_b64_tr_b16 reads of the dQ operand
+// (rows kk + 8g + q, 16-column blocks). The Q/dO layout lds_off<D> was 2-way on the latter.
+template <int D>
+PICO_DEV int kswz(int row) {
+  if constexpr (D == 64)
+    return (((row >> 1) & 1) << 1) ^ ((row >> 2) & 1) ^ (((row >> 3) & 1) << 2);
+  return ((row & 1) << 1) ^ (((row >> 1) & 1) << 2) ^ ((row >> 2) & 1) ^ (((row >> 3) & 1) << 3);
+}
+template <int D>
+PICO_DEV int kimg_off(int row, int chunk) {
+  return row * (D * 2) + 16 * (chunk ^ kswz<D>(row));
+}
+// 16x16x32 B operand K[k = row0 + 8 (l >> 4) + j][col0 + (l & 15)] from the K image (as lds_read_tr16)
+template <int D>
+PICO_DEV bf16x8 kimg_read_tr16(const char* base, int row0, int col0, int lane) {
+  const int g = lane >> 4, i = lane & 15;
+  const int q = i >> 2, p = i & 3;
+  const int col = col0 + 4 * p;
+  const int chunk = col >> 3, sub = (col & 7) * 2;
+  const int r0 = row0 + 8 * g + q;
+  const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(base + kimg_off<D>(r0, chunk) + sub));
+  const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(base + kimg_off<D>(r0 + 4, chunk) + sub));
+  typedef __attribute__((ext_vector_type(8))) short i16x8;
+  i16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
 }
 
 // delta[bh, q] = sum_d dO * O, lse2[bh, q] = LSE * log2(e); rows q in [Sq, Sq_pad) get delta = 0 and
@@ -122,7 +158,7 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(const pico_attn_args 
 }
 
 template <int D>
-constexpr int bwd_waves_per_eu() { return D == 64 ? 2 : 1; }
+constexpr int bwd_waves_per_eu() { return D == 64 ? PICO_BWD_WAVES_PER_EU_D64 : 1; }
 
 template <int D, bool CAUSAL>
 __global__ __launch_bounds__(512, bwd_waves_per_eu<D>()) void attn_bwd_kernel(
@@ -216,7 +252,7 @@ __global__ __launch_bounds__(512, bwd_waves_per_eu<D>()) void attn_bwd_kernel(
     const int row = id / CPR, ch = id % CPR;
     const int key = k0 + row;
     const u16x8 v = *reinterpret_cast<const u16x8*>(kg + (int64_t)min(key, Sk - 1) * a.k_strides[1] + ch * 8);
-    *reinterpret_cast<u16x8*>(kimg + lds_off<D>(row, ch)) = key < Sk ? v : (u16x8)0;
+    *reinterpret_cast<u16x8*>(kimg + kimg_off<D>(row, ch)) = key < Sk ? v : (u16x8)0;
   }
   bf16x8 vf[KS];
   {
@@ -267,7 +303,7 @@ __global__ __launch_bounds__(512, bwd_waves_per_eu<D>()) void attn_bwd_kernel(
         typedef __attribute__((ext_vector_type(8))) short i16x8;
         i16x8 av = {lo[0], lo[1], lo[2], lo[3], up[0], up[1], up[2], up[3]};
         if (PICO_BWD_DQ_UNROLL && kk >= kmax) av = (i16x8)0;
-        const bf16x8 bf = lds_read_tr16<D>(kimg, kk, di * 16, lane);
+        const bf16x8 bf = kimg_read_tr16<D>(kimg, kk, di * 16, lane);
         acc = mfma16(__builtin_bit_cast(bf16x8, av), bf, acc);
       }
       // every lane stores (rows past Sq go to a trash slot), so the per-tile count of vector-memory
@@ -312,7 +348,7 @@ __global__ __launch_bounds__(512, bwd_waves_per_eu<D>()) void attn_bwd_kernel(
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
         const bf16x8 qa = lds_read_b128(qs, lds_off<D>(r, 2 * ks + h));
-        const bf16x8 kbf = lds_read_b128(kimg, lds_off<D>(32 * wave + r, 2 * ks + h));
+        const bf16x8 kbf = lds_read_b128(kimg, kimg_off<D>(32 * wave + r, 2 * ks + h));
         s = mfma32(qa, kbf, s);
         const bf16x8 da = lds_read_b128(dos, lds_off<D>(r, 2 * ks + h));
         dp = mfma32(da, vf[ks], dp);
