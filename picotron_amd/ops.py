@@ -19,6 +19,7 @@ import math
 import os
 
 import torch
+from torch.optim.optimizer import register_optimizer_step_post_hook as _register_step_post_hook
 
 from . import _lib
 
@@ -288,6 +289,60 @@ def wgrad_accumulate(params, dy2, x2):
     return _plain_grads(params, torch.mm(dy2.t(), x2))
 
 
+# --------------------------------------------------------------------------------------------
+# Transposed weight copies for the dgrad GEMMs
+#
+# dx = dy W runs on hipBLASLt ~7-20 % slower in that (NN) form than the same product in the forward's
+# form F.linear(dy, W^T) against a contiguous W^T (measured on MI355X at M = 4096: gate_up 243 -> 213 us,
+# down 117 -> 97, qkv 104 -> 97, lm_head 634 -> 588; scripts/gemm_layout_probe.py). W^T is kept per
+# weight (bf16, +1 copy of the weights in HBM) and re-transposed only when the weights changed: after
+# any optimizer step (a global step post-hook bumps a generation; the fused AdamW does not bump the
+# parameters' version counters) or an in-place write that bumps a version counter.
+# refresh_weight_transposes() brings every cached copy up to date eagerly; MicroBatchGraph calls it
+# before each replay (a replayed graph runs no host code, so it could not notice stale copies).
+# --------------------------------------------------------------------------------------------
+_WT_GEN = [0]
+_WT_CACHE = {}  # W.data_ptr() -> [wt, key, W, params]
+_WT_HOOK = []
+
+
+def _bump_wt_gen(*_):
+    _WT_GEN[0] += 1
+
+
+def wt_dgrad_enabled():
+    """PICO_WT_DGRAD=0 computes dgrads as dy @ W (no transposed copies)."""
+    return os.getenv("PICO_WT_DGRAD", "1") != "0"
+
+
+def weight_t(W, params):
+    """Contiguous W^T ([K, N] for W [N, K]), up to date with the parameters `params` W is made of."""
+    if not _WT_HOOK:
+        _WT_HOOK.append(_register_step_post_hook(_bump_wt_gen))
+    key = (_WT_GEN[0],) + tuple(p._version for p in params)
+    ent = _WT_CACHE.get(W.data_ptr())
+    if ent is None or tuple(ent[0].shape) != (W.shape[1], W.shape[0]) or ent[0].dtype != W.dtype:
+        ent = [torch.empty((W.shape[1], W.shape[0]), dtype=W.dtype, device=W.device), None, W, params]
+        _WT_CACHE[W.data_ptr()] = ent
+    if ent[1] != key:
+        with torch.no_grad():
+            ent[0].copy_(W.t())
+        ent[1] = key
+    return ent[0]
+
+
+def refresh_weight_transposes():
+    for ent in list(_WT_CACHE.values()):
+        weight_t(ent[2], ent[3])
+
+
+def dgrad(dy2, W, params):
+    """dx = dy2 W for W [N, K] (the stacked weight of `params`)."""
+    if wt_dgrad_enabled():
+        return torch.nn.functional.linear(dy2, weight_t(W, params))
+    return torch.matmul(dy2, W)
+
+
 def _embedding_bwd_into(grad, ids, dy, scale):
     flat = ids.reshape(-1)
     sids, spos = torch.sort(flat, stable=True)
@@ -399,7 +454,7 @@ class _LinearFn(torch.autograd.Function):
     def backward(ctx, dy):
         x, w = ctx.saved_tensors
         dy2 = dy.reshape(-1, dy.shape[-1])
-        dx = torch.matmul(dy2, w).view(x.shape) if ctx.needs_input_grad[0] else None
+        dx = dgrad(dy2, w, (w,)).view(x.shape) if ctx.needs_input_grad[0] else None
         dw = wgrad_accumulate((w,), dy2, x.reshape(-1, x.shape[-1]))[0] if ctx.needs_input_grad[1] else None
         return dx, dw
 
@@ -466,7 +521,7 @@ class _GateUpSwiGLUFn(torch.autograd.Function):
             d = d.contiguous()
         dgu = torch.empty_like(gu)
         _swiglu_bwd(d, gu, gu[:, I:], dgu, dgu[:, I:], gu.shape[0], I, 2 * I, I)
-        dx = torch.matmul(dgu, W).view(ctx.xshape)
+        dx = dgrad(dgu, W, ctx.params).view(ctx.xshape)
         dwg, dwu = wgrad_accumulate(ctx.params, dgu, x2)
         return dx, dwg, dwu
 
@@ -623,7 +678,7 @@ class _QKVRopeAttentionFn(torch.autograd.Function):
                             dheads[:, :, :nh], dheads[:, :, nh:nh + nkv], dheads[:, :, nh + nkv:])
         dqk = dheads[:, :, : nh + nkv]
         _rope_launch(dqk, dqk, cos, sin, True)
-        dx = torch.matmul(dqkv, W).view(B, S, Hd)
+        dx = dgrad(dqkv, W, ctx.params).view(B, S, Hd)
         dwq, dwk, dwv = wgrad_accumulate(ctx.params, dqkv, x2)
         return dx, dwq, dwk, dwv, None, None, None, None, None
 

@@ -100,6 +100,8 @@ class MicroBatchGraph:
         self.loss_acc.zero_()
 
     def replay(self, input_ids, target_ids):
+        from . import ops
+        ops.refresh_weight_transposes()  # dgrad W^T copies are graph inputs: bring them up to date
         if self.graph is None:
             self._capture(input_ids, target_ids)
         self.inp.copy_(input_ids)

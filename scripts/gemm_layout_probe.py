@@ -1,0 +1,47 @@
+"""Probe hipBLASLt layout sensitivity for the SmolLM-1.7B training GEMMs (M = 4096 tokens):
+dgrad dx = dy @ W (NN) vs the same product in the forward's NT form F.linear(dy, W^T contiguous),
+and wgrad dW = dy^T @ x (TN) vs (x^T @ dy)^T variants. One JSON line per shape (microseconds)."""
+import json
+
+import torch
+import torch.nn.functional as F
+
+T, H, I, V = 4096, 2048, 8192, 49152
+SHAPES = {"qkv": (3 * H, H), "o": (H, H), "gate_up": (2 * I, H), "down": (H, I), "lm_head": (V, H)}
+
+
+def bench(fn, it=20, warm=5):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(it):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return round(s.elapsed_time(e) / it * 1e3, 1)
+
+
+def main():
+    torch.manual_seed(0)
+    for name, (N, K) in SHAPES.items():
+        x = torch.randn(T, K, device="cuda", dtype=torch.bfloat16)
+        w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.02
+        wt = w.t().contiguous()
+        dy = torch.randn(T, N, device="cuda", dtype=torch.bfloat16)
+        xt = x.t().contiguous()
+        dyt = dy.t().contiguous()
+        r = {"shape": name, "N": N, "K": K}
+        r["fwd_NT"] = bench(lambda: F.linear(x, w))
+        r["dgrad_NN"] = bench(lambda: dy @ w)
+        r["dgrad_NT_wt"] = bench(lambda: F.linear(dy, wt))
+        r["wgrad_TN"] = bench(lambda: dy.t() @ x)
+        r["wgrad_NN_dyt"] = bench(lambda: dyt @ x)
+        r["wgrad_NT_xt"] = bench(lambda: F.linear(dyt, xt))
+        r["transpose_w"] = bench(lambda: w.t().contiguous())
+        print(json.dumps(r), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -235,6 +235,41 @@ def test_wgrad_fusion_dp(golden_loss, monkeypatch):
         dist.destroy_process_group()
 
 
+def test_wt_dgrad_tracks_weights(golden_loss, monkeypatch):
+    """dgrads against the cached W^T copies (PICO_WT_DGRAD=1) == dy @ W within GEMM rounding, also
+    after fused-AdamW steps (which do not bump version counters) and after an in-place weight write;
+    a stale W^T would be off by the update (lr 1e-2, ~50 % of the init scale)."""
+    from conftest import rel_l2
+    from picotron_amd.model import build_llama
+    cfg = _cfg(golden_loss)
+    g = torch.Generator("cuda").manual_seed(17)
+    toks = [torch.randint(0, cfg.vocab_size, (2, 129), device="cuda", generator=g) for _ in range(3)]
+    V = cfg.vocab_size
+    res = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("PICO_WT_DGRAD", mode)
+        torch.manual_seed(7)
+        m = build_llama(cfg, "cuda", BF)
+        with torch.no_grad():
+            m.final_proj.weight.normal_(0, 0.02, generator=torch.Generator("cuda").manual_seed(1))
+        opt = torch.optim.AdamW(m.parameters(), lr=1e-2, fused=True)
+        grads = []
+        for i, t in enumerate(toks):
+            opt.zero_grad()
+            if i == 2:
+                with torch.no_grad():
+                    m.decoder_layers[0].mlp.up_proj.weight.mul_(1.5)
+            logits = m(t[:, :-1])
+            torch.nn.functional.cross_entropy(logits.reshape(-1, V).float(), t[:, 1:].reshape(-1)).backward()
+            grads.append({n: p.grad.float().clone() for n, p in m.named_parameters()})
+            opt.step()
+        torch.cuda.synchronize()
+        res[mode] = grads
+    for i in range(len(toks)):
+        for n in res["0"][i]:
+            assert rel_l2(res["1"][i][n].cpu(), res["0"][i][n].cpu()) < 2e-2, (i, n)
+
+
 def test_graph_replay_matches_eager(golden_loss):
     """MicroBatchGraph (HIP-graph replay of forward + CE + backward) gives the eager loop's loss and
     gradients bit for bit over a 3-micro-batch step, and a second step after an optimizer update."""
