@@ -25,6 +25,8 @@
  *                                 (ref train.py:46-49, picotron/pipeline_parallel/pipeline_parallel.py:68,98)
  *   pico_embedding_bwd        <- backward of F.embedding (ref picotron/model.py:223-224) + the micro-batch
  *                                 gradient accumulation (data_parallel.py:131 / autograd's grad += dW)
+ *   pico_transpose_bf16       <- no reference call: lays out x^T / W^T for the faster hipBLASLt forms of
+ *                                 the nn.Linear wgrad / dgrad GEMMs (ref picotron/model.py nn.Linear)
  *
  * Conventions: all pointers are device pointers allocated by the caller (kernels never
  * allocate); bf16 tensors are passed as raw 16-bit storage; `stream` is a hipStream_t
@@ -63,7 +65,8 @@ enum {
   PICO_K_EMBEDDING_BWD = 15,
   PICO_K_CE_FWD = 16,
   PICO_K_CE_BWD = 17,
-  PICO_K_COUNT = 18
+  PICO_K_TRANSPOSE = 18,
+  PICO_K_COUNT = 19
 };
 
 int pico_abi_version(void);
@@ -173,6 +176,12 @@ int pico_cross_entropy_fwd(const void* logits, int64_t ld, const int64_t* target
 int pico_cross_entropy_bwd(const void* logits, int64_t ld, const int64_t* target, const float* lse,
                            const float* grad_scale, void* dlogits, int64_t ldd, int64_t rows, int64_t vocab,
                            int64_t ignore_index, void* stream);
+
+/* ---- 2-D transpose ----
+ * dst[c][r] = src[r][c] for a [rows, cols] bf16 matrix with row stride ld_src into [cols, rows] with row
+ * stride ld_dst (elements). rows, cols, ld_src, ld_dst multiples of 8; pointers 16-byte aligned. */
+int pico_transpose_bf16(const void* src, int64_t ld_src, void* dst, int64_t ld_dst, int64_t rows, int64_t cols,
+                        void* stream);
 
 #ifdef __cplusplus
 }

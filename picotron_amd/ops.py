@@ -326,9 +326,35 @@ def weight_t(W, params):
         _WT_CACHE[W.data_ptr()] = ent
     if ent[1] != key:
         with torch.no_grad():
-            ent[0].copy_(W.t())
+            transpose_2d(W, out=ent[0])
         ent[1] = key
     return ent[0]
+
+
+def transpose_2d(x, out=None):
+    """Contiguous x^T ([C, R]) of a bf16 [R, C] matrix with unit column stride, on the HIP transpose
+    kernel (torch's strided copy runs at ~0.5 TB/s on these shapes)."""
+    R, C = x.shape
+    if out is None:
+        out = torch.empty((C, R), dtype=x.dtype, device=x.device)
+    ok = x.dtype == _BF16 and x.stride(1) == 1 and R % 8 == 0 and C % 8 == 0 and x.stride(0) % 8 == 0 and \
+        out.stride(1) == 1 and out.stride(0) % 8 == 0 and x.data_ptr() % 16 == 0 and out.data_ptr() % 16 == 0
+    if not ok:
+        out.copy_(x.t())
+        return out
+    _need(x, "x")
+    _lib.check(_lib.load().pico_transpose_bf16(_lib.ptr(x), x.stride(0), _lib.ptr(out), out.stride(0), R, C,
+                                               _lib.stream_of(x)), "pico_transpose_bf16")
+    return out
+
+
+def _wgrad_input(x2, n_out):
+    """What the backward keeps of a projection's input x2 [T, K] for its wgrad: x2 itself, or x2^T as a
+    transposed view of a contiguous [K, T] copy where hipBLASLt's "TT" wgrad form saves more than the
+    transpose costs (output width >= 3 K: qkv, gate|up, LM head; gemm_layout_probe.py --wgrad)."""
+    if os.getenv("PICO_XT_WGRAD", "1") != "0" and n_out >= 3 * x2.shape[1] and x2.is_cuda:
+        return transpose_2d(x2).t()
+    return x2
 
 
 def refresh_weight_transposes():
@@ -447,15 +473,17 @@ class _LinearFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w):
-        ctx.save_for_backward(x, w)
+        x2 = x.reshape(-1, x.shape[-1])
+        ctx.save_for_backward(_wgrad_input(x2, w.shape[0]) if ctx.needs_input_grad[1] else x2, w)
+        ctx.xshape = x.shape
         return torch.nn.functional.linear(x, w)
 
     @staticmethod
     def backward(ctx, dy):
-        x, w = ctx.saved_tensors
+        x2, w = ctx.saved_tensors
         dy2 = dy.reshape(-1, dy.shape[-1])
-        dx = dgrad(dy2, w, (w,)).view(x.shape) if ctx.needs_input_grad[0] else None
-        dw = wgrad_accumulate((w,), dy2, x.reshape(-1, x.shape[-1]))[0] if ctx.needs_input_grad[1] else None
+        dx = dgrad(dy2, w, (w,)).view(ctx.xshape) if ctx.needs_input_grad[0] else None
+        dw = wgrad_accumulate((w,), dy2, x2)[0] if ctx.needs_input_grad[1] else None
         return dx, dw
 
 
@@ -507,7 +535,7 @@ class _GateUpSwiGLUFn(torch.autograd.Function):
         gu = torch.matmul(x2, W.t())  # [T, 2I]
         h = torch.empty((x2.shape[0], I), dtype=x.dtype, device=x.device)
         _swiglu_fwd(gu, gu[:, I:], h, gu.shape[0], I, 2 * I, I)
-        ctx.save_for_backward(x2, gu, W)
+        ctx.save_for_backward(_wgrad_input(x2, 2 * I), gu, W)
         ctx.params = (w_gate, w_up)
         ctx.xshape = x.shape
         return h.view(*x.shape[:-1], I)
@@ -660,7 +688,7 @@ class _QKVRopeAttentionFn(torch.autograd.Function):
         q, k, v = heads[:, :, :nh], heads[:, :, nh:nh + nkv], heads[:, :, nh + nkv:]
         scale = 1.0 / math.sqrt(D)
         o, lse = attention_block_fwd(q, k, v, scale, causal)
-        ctx.save_for_backward(x2, W, qkv, o, lse, cos, sin)
+        ctx.save_for_backward(_wgrad_input(x2, N), W, qkv, o, lse, cos, sin)
         ctx.params = (wq, wk, wv)
         ctx.meta = (B, S, Hd, nh, nkv, D, causal, scale)
         return o.view(B, S, nh * D)

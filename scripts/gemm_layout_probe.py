@@ -43,5 +43,30 @@ def main():
         print(json.dumps(r), flush=True)
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and "--wgrad" not in __import__("sys").argv:
     main()
+
+
+def wgrad_main():
+    """wgrad as actually issued (beta = 1 accumulation into a bf16 grad) per input layout."""
+    torch.manual_seed(0)
+    for name, (N, K) in SHAPES.items():
+        x = torch.randn(T, K, device="cuda", dtype=torch.bfloat16)
+        dy = torch.randn(T, N, device="cuda", dtype=torch.bfloat16)
+        xt, dyt = x.t().contiguous(), dy.t().contiguous()
+        g = torch.zeros(N, K, device="cuda", dtype=torch.bfloat16)
+        r = {"shape": name, "N": N, "K": K}
+        r["acc_TN"] = bench(lambda: torch.addmm(g, dy.t(), x, out=g))
+        r["acc_NN_dyt"] = bench(lambda: torch.addmm(g, dyt, x, out=g))
+        r["acc_NT_dyt_xt"] = bench(lambda: torch.addmm(g, dyt, xt.t(), out=g))
+        r["acc_TT_dy_xt"] = bench(lambda: torch.addmm(g, dy.t(), xt.t(), out=g))
+        if name == "lm_head":
+            wt = torch.randn(K, N, device="cuda", dtype=torch.bfloat16)
+            r["dgradT_NN"] = bench(lambda: wt @ dyt)   # dx^T = W^T dlogits^T
+            r["dgrad_TN_dyt"] = bench(lambda: dyt.t() @ wt.t())
+        r["transpose_dy"] = bench(lambda: dy.t().contiguous())
+        print(json.dumps(r), flush=True)
+
+
+if __name__ == "__main__" and "--wgrad" in __import__("sys").argv:
+    wgrad_main()

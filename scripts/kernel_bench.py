@@ -33,6 +33,9 @@ def main(iters=50):
     ids = torch.randint(0, V, (4, 1024), device=dev)
     dy_emb = torch.randn(4, 1024, H, dtype=bf, device=dev)
     gemb = torch.zeros(V, H, dtype=bf, device=dev)
+    xt = torch.empty(H, T, dtype=bf, device=dev)
+    wgu = torch.randn(2 * I, H, dtype=bf, device=dev)
+    wgut = torch.empty(H, 2 * I, dtype=bf, device=dev)
 
     def run_norm():
         y, res = ops.rms_norm(x, w, 1e-5, residual=r, prenorm=True)
@@ -45,11 +48,16 @@ def main(iters=50):
                             ops._swiglu_bwd(dh, gu, gu[:, I:], dgu, dgu[:, I:], T, I, 2 * I, I)),
          [L.K_SWIGLU_FWD, L.K_SWIGLU_BWD]),
         ("embedding", lambda: ops._embedding_bwd_into(gemb, ids, dy_emb, 1.0), [L.K_EMBEDDING_BWD]),
+        ("transpose_x", lambda: ops.transpose_2d(x.detach(), out=xt), [L.K_TRANSPOSE]),
+        ("transpose_wgu", lambda: ops.transpose_2d(wgu, out=wgut), [L.K_TRANSPOSE]),
     ]
     work = {L.K_RMSNORM_FWD: 4 * T * H * 2 + 4 * T, L.K_RMSNORM_BWD: 4 * T * H * 2 + 4 * T,
             L.K_ROPE: 2 * T * 2 * NH * D * 2, L.K_SWIGLU_FWD: 3 * T * I * 2, L.K_SWIGLU_BWD: 5 * T * I * 2,
             L.K_EMBEDDING_BWD: T * H * 2 + 2 * T * H * 2}
+    tbytes = {"transpose_x": 2 * T * H * 2, "transpose_wgu": 2 * 2 * I * H * 2}
     for name, fn, kids in cases:
+        if L.K_TRANSPOSE in kids:
+            work[L.K_TRANSPOSE] = tbytes[name]
         for _ in range(3):
             fn()
         torch.cuda.synchronize()
@@ -61,7 +69,7 @@ def main(iters=50):
         for k in kids:
             ms, n = L.prof_collect(k)
             us = 1e3 * ms / max(n, 1)
-            out = {"kernel": L.KERNEL_NAMES[k], "avg_us": round(us, 2), "launches": n}
+            out = {"kernel": L.KERNEL_NAMES[k] + ("" if k != L.K_TRANSPOSE else ":" + name), "avg_us": round(us, 2), "launches": n}
             if k in work:
                 out["GB_s"] = round(work[k] / (us * 1e-6) / 1e9, 1)
                 out["frac_of_8TBs"] = round(out["GB_s"] / 8000, 3)

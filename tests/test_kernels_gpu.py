@@ -371,3 +371,22 @@ def test_cross_entropy_matches_torch(V, ignore):
     assert float(logits.grad[~keep].abs().sum()) == 0.0
     t_loss = torch.nn.functional.cross_entropy(logits.detach(), tgt)
     assert abs(float(t_loss) - float(loss)) <= 1.6e-2 * abs(float(ref)) + 2e-3
+
+
+# ------------------------------------------------------------------------------------------ transpose
+@pytest.mark.parametrize("R,C,ld_pad", [(4096, 2048, 0), (6144, 2048, 0), (2048, 49152, 0), (72, 8, 0),
+                                        (8, 136, 0), (200, 264, 16), (64, 64, 8)])
+def test_transpose_bit_exact(R, C, ld_pad):
+    """pico_transpose_bf16 == x.t() bit for bit, incl. partial tiles and padded row strides on both sides
+    (the padding of the output is left untouched)."""
+    from picotron_amd import ops
+    torch.manual_seed(R + C)
+    base = torch.randn(R, C + ld_pad, device=DEV).to(BF)
+    x = base[:, :C]
+    out_base = torch.full((C, R + ld_pad), 7.0, device=DEV, dtype=BF)
+    out = out_base[:, :R]
+    ops.transpose_2d(x, out=out)
+    assert torch.equal(out, x.t())
+    if ld_pad:
+        assert bool((out_base[:, R:] == 7.0).all())
+    assert torch.equal(ops.transpose_2d(x), x.t().contiguous())
