@@ -26,21 +26,27 @@
 #include "attn_common.h"
 
 // Build-time variants (A/B measurement only; the shipped defaults are the measured-best):
-//   PICO_BWD_DQ_UNROLL: dQ key steps fully unrolled + predicated (1) or a runtime-bounded loop (0)
-#ifndef PICO_BWD_DQ_UNROLL
-#define PICO_BWD_DQ_UNROLL 0
-#endif
 //   PICO_BWD_WAVES_PER_EU_D64: register budget for D = 64 (2: <= 256 VGPRs, one 512-thread workgroup
 //     per CU; 4: <= 128 VGPRs, two per CU — their LDS (75 KiB each) fits)
 #ifndef PICO_BWD_WAVES_PER_EU_D64
 #define PICO_BWD_WAVES_PER_EU_D64 2
 #endif
+//   PICO_BWD_STAMP: diagnostic build — workgroup 0 records s_memtime stamps per (wave, tile, phase) in LDS
+//     and dumps them after the trash slot (workspace grows by STAMP_BYTES); results unchanged
+#ifndef PICO_BWD_STAMP
+#define PICO_BWD_STAMP 0
+#endif
+//   PICO_BWD_STAGGER: waves 4-7 run the dQ tile of t-1 BEFORE tile t's S/dP (1) or after (0)
+#ifndef PICO_BWD_STAGGER
+#define PICO_BWD_STAGGER 1
+#endif
 
 namespace {
 
 constexpr int BK = 256;  // keys per workgroup
+constexpr int STAMP_TILES = 40, STAMP_PH = 6;
+constexpr int64_t STAMP_BYTES = PICO_BWD_STAMP ? 8 * STAMP_TILES * STAMP_PH * 8 : 0;
 constexpr int BQ = 32;   // query rows per tile
-constexpr int NBUF = 3;  // ring slots (prefetch distance 2)
 
 template <int D>
 struct BwdCfg {
@@ -50,13 +56,37 @@ struct BwdCfg {
   static constexpr int LSD = 1024;              // LSE*log2e [32] | delta [32] (one DMA piece)
   static constexpr int SLOT = 2 * QIMG + LSD;
   static constexpr int KIMG = BK * RB;
-  static constexpr int DSIMG = BK * BQ * 2;     // dS^T [key][q] bf16, 64-B rows
-  static constexpr int SMEM = KIMG + NBUF * SLOT + DSIMG;
+  static constexpr int DSIMG = BK * BQ * 2;     // dS^T [key][q] bf16, 64-B rows (two: tiles t, t-1)
+  static constexpr int NBUF = D == 64 ? 4 : 3;  // ring slots
+  static constexpr int PD = NBUF - 1;           // prefetch distance (tiles)
+  static constexpr int SMEM = KIMG + NBUF * SLOT + 2 * DSIMG;
   static constexpr int RPP = 1024 / RB;         // image rows per 1-KiB DMA piece
   static constexpr int NQP = QIMG / 1024;       // pieces per Q (or dO) tile
   static constexpr int NP = 2 * NQP + 1;        // pieces per tile
   static constexpr int NPW = (NP + 7) / 8;      // max pieces per wave
 };
+
+// One LDS-DMA piece (16 B per lane, lane-linear at the wave-uniform LDS byte address lds_base) issued
+// from inline asm: the compiler does not see it as an LDS write, so it inserts none of its
+// conservative `s_waitcnt vmcnt(0)` before the loop's LDS reads and writes (which would expose the
+// full HBM latency of the piece just issued, every tile). The kernel's counted waits + barrier order
+// the pieces against their readers; ring slots are never touched while a piece for them is in flight.
+// Address = wave-uniform base (SGPR pair) + per-lane 32-bit byte offset.
+PICO_DEV void dma_piece(const void* base, unsigned voff, unsigned lds_base) {
+  const uint64_t p = (uint64_t)(uintptr_t)base;  // wave-uniform by construction; make it an SGPR pair
+  const uint64_t sbase = (uint64_t)(unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)p) |
+                         ((uint64_t)(unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(p >> 32)) << 32);
+  asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase), "s"(lds_base) : "memory");
+}
+
+// Workgroup barrier without the fence __syncthreads() implies (whose release semantics make the
+// compiler drain vmcnt(0) — the in-flight DMA and dQ stores — before every barrier). LDS writes are
+// drained (lgkmcnt(0)); the asm memory clobbers keep memory accesses from moving across it.
+PICO_DEV void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
 
 // s_waitcnt vmcnt(n) for a wave-uniform runtime n (the immediate must be a constant)
 PICO_DEV void wait_vmcnt(int n) {
@@ -170,12 +200,21 @@ __global__ __launch_bounds__(512, bwd_waves_per_eu<D>()) void attn_bwd_kernel(
   __shared__ __attribute__((aligned(16))) char smem[C::SMEM];
   char* kimg = smem;
   char* ring = smem + C::KIMG;
-  char* dsimg0 = smem + C::KIMG + NBUF * C::SLOT;  // dS^T [key][q] of the current tile
+  char* dsimg0 = smem + C::KIMG + C::NBUF * C::SLOT;  // dS^T [key][q] images of tiles t (t % 2), t - 1
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (scalar branches)
   const int r = lane & 31, h = lane >> 5;
   const int Sq = (int)a.seqlen_q, Sk = (int)a.seqlen_k;
+#if PICO_BWD_STAMP
+  __shared__ unsigned long long stamps[D == 64 ? 8 * STAMP_TILES * STAMP_PH : 1];  // D = 64 only (LDS)
+  auto stamp = [&](int t, int ph) __attribute__((always_inline)) {
+    const unsigned long long v = __builtin_amdgcn_s_memtime();
+    if (D == 64 && lane == 0 && t < STAMP_TILES) stamps[(wave * STAMP_TILES + t) * STAMP_PH + ph] = v;
+  };
+#else
+  auto stamp = [](int, int) __attribute__((always_inline)) {};
+#endif
   const int Hq = (int)a.heads_q;
   const int G = (int)(a.heads_q / a.heads_kv);
 
@@ -220,32 +259,55 @@ __global__ __launch_bounds__(512, bwd_waves_per_eu<D>()) void attn_bwd_kernel(
       pc_dst[i] = 2 * C::QIMG;
     }
   }
-  auto issue = [&](int t) __attribute__((always_inline)) {
-    const int hq = hk * G + t / nqt;
-    const int q0 = qstart + (t % nqt) * BQ;
-    char* slot = ring + (unsigned)(t % NBUF) * (unsigned)C::SLOT;
+  // tile coordinates (query head, first query row), advanced incrementally (no per-tile divisions)
+  struct Tc {
+    int hq, q0;
+  };
+  const int qend = qstart + nqt * BQ;
+  auto advance = [&](Tc& c) __attribute__((always_inline)) {
+    c.q0 += BQ;
+    if (c.q0 >= qend) {
+      c.q0 = qstart;
+      ++c.hq;
+    }
+  };
+  auto next_slot = [](int si) __attribute__((always_inline)) { return si + 1 == C::NBUF ? 0 : si + 1; };
+  const bf16_t* qbase = (const bf16_t*)a.q + b * a.q_strides[0];
+  const bf16_t* dobase = (const bf16_t*)a.dout + b * a.do_strides[0];
+  const unsigned delta_off = (unsigned)((const char*)delta_g - (const char*)lse2_g);  // same workspace
+  const unsigned ring_lds = (unsigned)__builtin_amdgcn_readfirstlane((int)lds_addr(smem)) + (unsigned)C::KIMG;
+  auto issue = [&](int si, Tc c) __attribute__((always_inline)) {
+    const int hq = c.hq, q0 = c.q0;
     const bool full = q0 + BQ <= Sq;
 #pragma unroll
     for (int i = 0; i < C::NPW; ++i) {
       if (i < my_np) {
-        const void* src;
-        if (pc_kind[i] == 2) {
-          const float* base = pc_col[i] ? delta_g : lse2_g;
-          src = base + ((int64_t)b * Hq + hq) * sq_pad + q0 + pc_row[i];
+        const void* base;
+        unsigned off;
+        if (pc_kind[i] == 2) {  // lanes 0-7: LSE*log2e, 8-15: delta (pc_col), 4 rows each
+          base = lse2_g + ((int64_t)b * Hq + hq) * sq_pad + q0;
+          off = (unsigned)pc_row[i] * 4u + (pc_col[i] ? delta_off : 0u);
         } else {
-          const int q = full ? q0 + pc_row[i] : min(q0 + pc_row[i], Sq - 1);
-          src = pc_kind[i] == 0
-                    ? (const bf16_t*)a.q + b * a.q_strides[0] + hq * a.q_strides[2] + (int64_t)q * a.q_strides[1] + pc_col[i]
-                    : (const bf16_t*)a.dout + b * a.do_strides[0] + hq * a.do_strides[2] + (int64_t)q * a.do_strides[1] +
-                          pc_col[i];
+          const int dq = full ? pc_row[i] : min(q0 + pc_row[i], Sq - 1) - q0;  // row within the tile
+          if (pc_kind[i] == 0) {
+            base = qbase + hq * a.q_strides[2] + (int64_t)q0 * a.q_strides[1];
+            off = (unsigned)(dq * a.q_strides[1] + pc_col[i]) * 2u;
+          } else {
+            base = dobase + hq * a.do_strides[2] + (int64_t)q0 * a.do_strides[1];
+            off = (unsigned)(dq * a.do_strides[1] + pc_col[i]) * 2u;
+          }
         }
-        __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(slot + pc_dst[i]), 16, 0, 0);
+        dma_piece(base, off, ring_lds + (unsigned)si * (unsigned)C::SLOT + pc_dst[i]);
       }
     }
   };
-  // first two tiles go out before the K/V prologue loads
-  if (ntiles > 0) issue(0);
-  if (ntiles > 1) issue(1);
+  // the first PD tiles go out before the K/V prologue loads; nxt = coordinates of tile PD afterwards
+  Tc nxt = {hk * G, qstart};
+#pragma unroll
+  for (int j = 0; j < C::PD; ++j) {
+    if (j < ntiles) issue(j, nxt);
+    advance(nxt);
+  }
 
   // ---- K block -> LDS image; V fragments -> registers (B operand of dP = dO V^T) ----
   for (int id = threadIdx.x; id < BK * CPR; id += 512) {
@@ -272,140 +334,194 @@ __global__ __launch_bounds__(512, bwd_waves_per_eu<D>()) void attn_bwd_kernel(
     dv[dt] = (f32x16)0.f;
   }
 
+  auto slot_of = [&](int si) __attribute__((always_inline)) {
+    return (const char*)(ring + (unsigned)si * (unsigned)C::SLOT);
+  };
+  // causal: a wave whose keys all lie past the tile's last query row has nothing to do for it
+  auto active = [&](int q0) __attribute__((always_inline)) { return !CAUSAL || kw <= q0 + BQ - 1; };
+
+  // S[q][key] and dP[q][key] of tile t: A = Q / dO rows (LDS), B = K^T (LDS) / V^T (registers)
+  auto sdp = [&](int si, f32x16& s, f32x16& dp) __attribute__((always_inline)) {
+    const char* qs = slot_of(si);
+    const char* dos = qs + C::QIMG;
+    s = (f32x16)0.f;
+    dp = (f32x16)0.f;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const bf16x8 qa = lds_read_b128(qs, lds_off<D>(r, 2 * ks + h));
+      const bf16x8 kbf = lds_read_b128(kimg, kimg_off<D>(32 * wave + r, 2 * ks + h));
+      s = mfma32(qa, kbf, s);
+      const bf16x8 da = lds_read_b128(dos, lds_off<D>(r, 2 * ks + h));
+      dp = mfma32(da, vf[ks], dp);
+    }
+  };
+
+  // P = exp2(S * scale*log2e - LSE*log2e) (in s), dS = P * (dP - delta) (in dp); then
+  // dV[key][d] += P^T dO, dK[key][d] += dS^T Q (k index = the tile's query rows)
+  auto softmax_dkdv = [&](int si, int q0, f32x16& s, f32x16& dp) __attribute__((always_inline)) {
+    const char* qs = slot_of(si);
+    const char* dos = qs + C::QIMG;
+    const float* lsd = (const float*)(qs + 2 * C::QIMG);
+    // rows of this lane's accumulator registers: q = 8g + 4h + (0..3), g = 0..3
+    f32x4 l2[4], dl[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      l2[g] = *reinterpret_cast<const f32x4*>(lsd + 8 * g + 4 * h);
+      dl[g] = *reinterpret_cast<const f32x4*>(lsd + 32 + 8 * g + 4 * h);
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s[i] = fast_exp2(__builtin_fmaf(s[i], scale_log2, -l2[i >> 2][i & 3]));
+    if ((CAUSAL && kw + 31 > q0) || (k0 + BK > Sk)) {  // wave-uniform
+      // causal: key > q  <=>  (i&3) + 8(i>>2) < rel;  padding keys: key >= Sk
+      const int rel = CAUSAL ? my_key - q0 - 4 * h : -1;
+      const bool kill_all = my_key >= Sk;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) s[i] = ((i & 3) + 8 * (i >> 2) < rel || kill_all) ? 0.f : s[i];
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dp[i] = s[i] * (dp[i] - dl[i >> 2][i & 3]);
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      float pv[8], sv[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        pv[j] = s[8 * st + j];
+        sv[j] = dp[8 * st + j];
+      }
+      const bf16x8 pf = pack_frag(pv);
+      const bf16x8 sf = pack_frag(sv);
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        const bf16x8 dof = lds_read_tr32<D>(dos, 16 * st, 32 * dt, lane);
+        dv[dt] = mfma32(pf, dof, dv[dt]);
+        const bf16x8 qf = lds_read_tr32<D>(qs, 16 * st, 32 * dt, lane);
+        dk[dt] = mfma32(sf, qf, dk[dt]);
+      }
+    }
+  };
+
+  // dS^T image [key][q] (bf16) of tile t: registers 4g..4g+3 are q = 8g + 4h + 0..3 -> one 8-B store each
+  auto ds_write = [&](int par, const f32x16& dp) __attribute__((always_inline)) {
+    char* dsimg = dsimg0 + (unsigned)par * (unsigned)C::DSIMG;
+    const int krow = 32 * wave + r;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      u16x4 w;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) w[j] = f2bf(dp[4 * g + j]);
+      *reinterpret_cast<u16x4*>(dsimg + ds_img_off(krow, 8 * g + 4 * h)) = w;
+    }
+  };
+
   // dQ partial [q][d] = scale * dS[q][:] K[:][d] over this block's keys for tile t (16x16 tiles, one
   // (or two, D=128) per wave; both operands by transposed reads), stored fp32 into the key block's slab.
-  auto dq_tile = [&](int t) __attribute__((always_inline)) {
-    const int hq = hk * G + t / nqt;
-    const int q0 = qstart + (t % nqt) * BQ;
-    const char* dsimg = dsimg0;
+  // D = 64: the 16x16x32 key steps are software-pipelined, step i+1's four transposed reads issued
+  // before step i's MFMA (reads of steps past kmax are harmless: in-bounds LDS, never consumed).
+  auto dq_tile = [&](int par, Tc c) __attribute__((always_inline)) {
+    const char* dsimg = dsimg0 + (unsigned)par * (unsigned)C::DSIMG;
     constexpr int NT = (BQ / 16) * (D / 16);
     int kmax = min(BK, Sk - k0);
-    if (CAUSAL) kmax = min(kmax, q0 + BQ - k0);
+    if (CAUSAL) kmax = min(kmax, c.q0 + BQ - k0);
+    const int nst = (kmax + 31) >> 5;  // key steps (wave-uniform)
     const int g16 = lane >> 4, i16 = lane & 15;
+    typedef __attribute__((ext_vector_type(8))) short i16x8;
 #pragma unroll
     for (int tt = 0; tt < NT / 8; ++tt) {
       const int tl = wave + 8 * tt;
       const int qi = tl / (D / 16), di = tl % (D / 16);
-      f32x4 acc = (f32x4)0.f;
-      // all BK/32 key steps unrolled so the transposed LDS reads issue back to back; steps past
-      // kmax read (stale) LDS and are zeroed in the A operand instead of branched around
-#if PICO_BWD_DQ_UNROLL
-#pragma unroll
-      for (int kk = 0; kk < BK; kk += 32) {
-#else
-      for (int kk = 0; kk < kmax; kk += 32) {
-#endif
-        // A = dS[q = 16 qi + (lane & 15)][key = kk + 8 g16 + j]: transposed read of the [key][q] image
-        const int row = kk + 8 * g16 + (i16 >> 2);
-        const int qc = 16 * qi + 4 * (i16 & 3);
+      const int qc = 16 * qi + 4 * (i16 & 3);
+      // A = dS[q = 16 qi + (lane & 15)][key = kk + 8 g16 + j]: transposed read of the [key][q] image
+      auto load = [&](int i, bf16x8& av, bf16x8& bv) __attribute__((always_inline)) {
+        const int row = 32 * i + 8 * g16 + (i16 >> 2);
         const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(dsimg + ds_img_off(row, qc)));
         const i16x4 up = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(dsimg + ds_img_off(row + 4, qc)));
-        typedef __attribute__((ext_vector_type(8))) short i16x8;
-        i16x8 av = {lo[0], lo[1], lo[2], lo[3], up[0], up[1], up[2], up[3]};
-        if (PICO_BWD_DQ_UNROLL && kk >= kmax) av = (i16x8)0;
-        const bf16x8 bf = kimg_read_tr16<D>(kimg, kk, di * 16, lane);
-        acc = mfma16(__builtin_bit_cast(bf16x8, av), bf, acc);
+        const i16x8 v = {lo[0], lo[1], lo[2], lo[3], up[0], up[1], up[2], up[3]};
+        av = __builtin_bit_cast(bf16x8, v);
+        bv = kimg_read_tr16<D>(kimg, 32 * i, di * 16, lane);
+      };
+      f32x4 acc = (f32x4)0.f;
+      if constexpr (D == 64) {
+        bf16x8 a0, b0, a1, b1;
+        load(0, a0, b0);
+#pragma unroll
+        for (int i = 0; i < BK / 32; i += 2) {
+          load(i + 1, a1, b1);
+          if (i < nst) acc = mfma16(a0, b0, acc);
+          if (i + 2 < BK / 32) load(i + 2, a0, b0);
+          if (i + 1 < nst) acc = mfma16(a1, b1, acc);
+        }
+      } else {  // D = 128: no registers for the second operand set
+        for (int i = 0; i < nst; ++i) {
+          bf16x8 a0, b0;
+          load(i, a0, b0);
+          acc = mfma16(a0, b0, acc);
+        }
       }
       // every lane stores (rows past Sq go to a trash slot), so the per-tile count of vector-memory
       // instructions is fixed and the ring's vmcnt waits stay exact
-      float* dst = dq_part + kb * slab + (int64_t)b * Sq * Hq * D + hq * D + di * 16 + i16;
+      float* dst = dq_part + kb * slab + (int64_t)b * Sq * Hq * D + c.hq * D + di * 16 + i16;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int q = q0 + qi * 16 + 4 * g16 + j;
+        const int q = c.q0 + qi * 16 + 4 * g16 + j;
         float* p = q < Sq ? dst + (int64_t)q * Hq * D : trash + lane;
         *p = acc[j] * scale;
       }
     }
   };
 
+  // One barrier per tile: iteration t computes tile t (S/dP -> P/dS -> dV/dK, dS image t % 2) and the
+  // dQ tile of t-1, whose dS image the barrier published. The two waves sharing a SIMD (w, w + 4) run
+  // them in opposite orders, so one's S/dP and dV/dK MFMAs overlap the other's LDS-latency-bound dQ
+  // steps and softmax VALU instead of both waves contending for the same unit in lockstep.
+  // Per-wave vector-memory ops in issue order, iteration j: DMA pieces of tile j+PD, dQ stores of j-1.
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // K image and the prologue tiles visible
+  constexpr int NST = 4 * ((BQ / 16) * (D / 16) / 8);  // dQ stores per wave per tile
+  const bool dq_first = PICO_BWD_STAGGER && D == 64 && wave >= 4;  // D = 128: no registers to spare
+  Tc cur = {hk * G, qstart}, prev = cur;
+  int si_cur = 0, si_nxt = C::PD;  // ring slots of tiles t and t + PD
   for (int t = 0; t < ntiles; ++t) {
-    // this wave's pieces of tile t landed (tile t+1's stay in flight), then everyone's (barrier);
-    // the barrier also retires every read of iteration t-1 (ring slot (t+2) % 3, dS image)
-    {
-      // vector-memory ops this wave issued after tile t's DMA pieces: dQ stores of tile t-2, the
-      // pieces of tile t+1, dQ stores of tile t-1 (issue order) — they may stay in flight
-      constexpr int NST = 4 * ((BQ / 16) * (D / 16) / 8);
-      int younger = 0;
-      if (t >= 2) younger += NST;
-      if (t + 1 < ntiles) younger += my_np;
-      if (t >= 1) younger += NST;
+    stamp(t, 0);
+    // my pieces of tile t landed: issued in iteration j0 = t - PD, or in the prologue (j0 < 0)
+    const int j0 = t - C::PD;
+    if (j0 >= 0) {
+      int younger = j0 >= 1 ? NST : 0;
+      for (int j = j0 + 1; j < t; ++j) younger += (j + C::PD < ntiles ? my_np : 0) + (j >= 1 ? NST : 0);
       wait_vmcnt(younger);
     }
-    __syncthreads();
-    if (t + 2 < ntiles) issue(t + 2);
-
-    const int hq = hk * G + t / nqt;
-    const int q0 = qstart + (t % nqt) * BQ;
-    const char* slot = ring + (unsigned)(t % NBUF) * (unsigned)C::SLOT;
-    const char* qs = slot;
-    const char* dos = slot + C::QIMG;
-    const float* lsd = (const float*)(slot + 2 * C::QIMG);
-
-    const bool active = !CAUSAL || kw <= q0 + BQ - 1;
-    if (active) {
-      // S[q][key] and dP[q][key]: A = Q / dO rows (LDS), B = K^T (LDS) / V^T (registers)
-      f32x16 s = (f32x16)0.f, dp = (f32x16)0.f;
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        const bf16x8 qa = lds_read_b128(qs, lds_off<D>(r, 2 * ks + h));
-        const bf16x8 kbf = lds_read_b128(kimg, kimg_off<D>(32 * wave + r, 2 * ks + h));
-        s = mfma32(qa, kbf, s);
-        const bf16x8 da = lds_read_b128(dos, lds_off<D>(r, 2 * ks + h));
-        dp = mfma32(da, vf[ks], dp);
-      }
-      // rows of this lane's accumulator registers: q = 8g + 4h + (0..3), g = 0..3
-      f32x4 l2[4], dl[4];
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        l2[g] = *reinterpret_cast<const f32x4*>(lsd + 8 * g + 4 * h);
-        dl[g] = *reinterpret_cast<const f32x4*>(lsd + 32 + 8 * g + 4 * h);
-      }
-      // P = exp2(S * scale*log2e - LSE*log2e) (in s), dS = P * (dP - delta) (in dp); lane: key my_key
-#pragma unroll
-      for (int i = 0; i < 16; ++i) s[i] = fast_exp2(__builtin_fmaf(s[i], scale_log2, -l2[i >> 2][i & 3]));
-      if ((CAUSAL && kw + 31 > q0) || (k0 + BK > Sk)) {  // wave-uniform
-        // causal: key > q  <=>  (i&3) + 8(i>>2) < rel;  padding keys: key >= Sk
-        const int rel = CAUSAL ? my_key - q0 - 4 * h : -1;
-        const bool kill_all = my_key >= Sk;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) s[i] = ((i & 3) + 8 * (i >> 2) < rel || kill_all) ? 0.f : s[i];
-      }
-#pragma unroll
-      for (int i = 0; i < 16; ++i) dp[i] = s[i] * (dp[i] - dl[i >> 2][i & 3]);
-      // dV[key][d] += P^T dO ; dK[key][d] += dS^T Q   (k index = query rows of the tile)
-#pragma unroll
-      for (int st = 0; st < 2; ++st) {
-        float pv[8], sv[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          pv[j] = s[8 * st + j];
-          sv[j] = dp[8 * st + j];
-        }
-        const bf16x8 pf = pack_frag(pv);
-        const bf16x8 sf = pack_frag(sv);
-#pragma unroll
-        for (int dt = 0; dt < DT; ++dt) {
-          const bf16x8 dof = lds_read_tr32<D>(dos, 16 * st, 32 * dt, lane);
-          dv[dt] = mfma32(pf, dof, dv[dt]);
-          const bf16x8 qf = lds_read_tr32<D>(qs, 16 * st, 32 * dt, lane);
-          dk[dt] = mfma32(sf, qf, dk[dt]);
-        }
-      }
-      // dS^T image [key][q] (bf16): registers 4g..4g+3 are q = 8g + 4h + 0..3 -> one 8-B store each
-      char* dsimg = dsimg0;
-      const int krow = 32 * wave + r;
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        u16x4 w;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) w[j] = f2bf(dp[4 * g + j]);
-        *reinterpret_cast<u16x4*>(dsimg + ds_img_off(krow, 8 * g + 4 * h)) = w;
-      }
+    // everyone's pieces of tile t visible, dS(t-1) visible, reads of slot (t-1) % NBUF and of
+    // dS image t % 2 (dQ of t-2) retired
+    lds_barrier();
+    stamp(t, 1);
+    if (t + C::PD < ntiles) issue(si_nxt, nxt);
+    if (dq_first && t >= 1) dq_tile((t - 1) & 1, prev);
+    stamp(t, 2);
+    if (active(cur.q0)) {
+      f32x16 s, dp;
+      sdp(si_cur, s, dp);
+      softmax_dkdv(si_cur, cur.q0, s, dp);
+      stamp(t, 3);
+      ds_write(t & 1, dp);
     }
-    __syncthreads();  // dS visible
-    dq_tile(t);
+    stamp(t, 4);
+    if (!dq_first && t >= 1) dq_tile((t - 1) & 1, prev);
+    stamp(t, 5);
+    prev = cur;
+    advance(cur);
+    advance(nxt);
+    si_cur = next_slot(si_cur);
+    si_nxt = next_slot(si_nxt);
   }
+  lds_barrier();
+  if (ntiles > 0) dq_tile((ntiles - 1) & 1, prev);
 
+#if PICO_BWD_STAMP
+  if (D == 64 && blockIdx.x == 0) {
+    unsigned long long* out = reinterpret_cast<unsigned long long*>(trash + 64);
+    for (int i = lane; i < STAMP_TILES * STAMP_PH; i += 64)
+      out[wave * STAMP_TILES * STAMP_PH + i] = stamps[wave * STAMP_TILES * STAMP_PH + i];
+  }
+#endif
   // ---- epilogue: dK = scale * acc, dV = acc; lane holds d = 32 dt + r, keys kw + acc_row(i, h) ----
   bf16_t* dkg = (bf16_t*)a.dk + b * a.dk_strides[0] + hk * a.dk_strides[2];
   bf16_t* dvg = (bf16_t*)a.dv + b * a.dv_strides[0] + hk * a.dv_strides[2];
@@ -538,7 +654,7 @@ int64_t pico_attn_bwd_workspace_bytes(const pico_attn_args* a) {
   // lse2, delta [B*Hq*Sq_pad] fp32 + one fp32 dQ partial slab [B, Sq, Hq, D] per 256-key block
   const int64_t nkb = (a->seqlen_k + BK - 1) / BK;
   // + 64 floats of trash for the dQ stores of padded query rows
-  return (2 * lsd_floats(a) + nkb * a->batch * a->seqlen_q * a->heads_q * a->head_dim + 64) * 4;
+  return (2 * lsd_floats(a) + nkb * a->batch * a->seqlen_q * a->heads_q * a->head_dim + 64) * 4 + STAMP_BYTES;
 }
 
 int pico_attn_bwd(const pico_attn_args* a, void* stream) {
