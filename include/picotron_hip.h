@@ -92,6 +92,15 @@ int64_t pico_rmsnorm_bwd_workspace_bytes(int64_t rows, int64_t cols);
 int pico_rmsnorm_bwd(const void* dy, const void* dresidual, const void* x, const void* weight,
                      const float* rstd, void* dx, void* dweight, void* workspace, int64_t rows,
                      int64_t cols, void* stream);
+/* As pico_rmsnorm_bwd, with the weight gradient's micro-batch accumulation folded in (the
+ * reference's AccumulateGrad `grad += dw` at DP = 1 / DataParallelBucket's `main_grad += grad`,
+ * ref picotron/data_parallel/data_parallel.py:131, and the bucket's /W, bucket.py:30):
+ *   dw_mode 0: dweight (bf16)  = sum                      (== pico_rmsnorm_bwd)
+ *   dw_mode 1: dweight (bf16)  = bf16(dweight + sum)       (one rounding)
+ *   dw_mode 2: dweight (fp32)  = (dweight + sum) * dw_scale */
+int pico_rmsnorm_bwd_acc(const void* dy, const void* dresidual, const void* x, const void* weight,
+                         const float* rstd, void* dx, void* dweight, int dw_mode, float dw_scale,
+                         void* workspace, int64_t rows, int64_t cols, void* stream);
 
 /* ---- RoPE, rotate-half (non-interleaved) layout ----
  * x, out: [batch, seqlen, heads, head_dim] bf16 with element strides (batch, seq, head) and

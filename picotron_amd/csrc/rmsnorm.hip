@@ -182,8 +182,10 @@ int launch_rmsnorm_bwd(const void* dy, const void* dres, const void* x, const vo
 // dw[col] = sum over the workgroup partials, in a fixed order (deterministic): a 256-thread
 // workgroup covers 32 columns x 8 row-slices; each thread sums its slice (loads coalesced across the
 // 32 columns), then the 8 slices are combined through LDS in slice order.
-__global__ __launch_bounds__(256) void rmsnorm_dw_kernel(const float* __restrict__ part, bf16_t* __restrict__ dw, int nblk,
-                                                         int cols) {
+// MODE 0: dw (bf16) = sum; 1: dw (bf16) = bf16(dw + sum); 2: dw (fp32) = (dw + sum) * scale
+template <int MODE>
+__global__ __launch_bounds__(256) void rmsnorm_dw_kernel(const float* __restrict__ part, void* __restrict__ dw, int nblk,
+                                                         int cols, float scale) {
   __shared__ float red[8][32];
   const int c = threadIdx.x & 31, sl = threadIdx.x >> 5;
   const int col = blockIdx.x * 32 + c;
@@ -198,7 +200,15 @@ __global__ __launch_bounds__(256) void rmsnorm_dw_kernel(const float* __restrict
     float t = red[0][c];
 #pragma unroll
     for (int k = 1; k < 8; ++k) t += red[k][c];
-    dw[col] = f2bf(t);
+    if constexpr (MODE == 0) {
+      ((bf16_t*)dw)[col] = f2bf(t);
+    } else if constexpr (MODE == 1) {
+      bf16_t* p = (bf16_t*)dw + col;
+      *p = f2bf(bf2f(*p) + t);
+    } else {
+      float* p = (float*)dw + col;
+      *p = (*p + t) * scale;
+    }
   }
 }
 
@@ -258,7 +268,14 @@ int64_t pico_rmsnorm_bwd_workspace_bytes(int64_t rows, int64_t cols) {
 
 int pico_rmsnorm_bwd(const void* dy, const void* dresidual, const void* x, const void* weight, const float* rstd,
                      void* dx, void* dweight, void* workspace, int64_t rows, int64_t cols, void* stream) {
+  return pico_rmsnorm_bwd_acc(dy, dresidual, x, weight, rstd, dx, dweight, 0, 1.f, workspace, rows, cols, stream);
+}
+
+int pico_rmsnorm_bwd_acc(const void* dy, const void* dresidual, const void* x, const void* weight, const float* rstd,
+                         void* dx, void* dweight, int dw_mode, float dw_scale, void* workspace, int64_t rows,
+                         int64_t cols, void* stream) {
   PICO_REQUIRE(dy && x && weight && rstd && dx && dweight && workspace, "pico_rmsnorm_bwd: null pointer");
+  PICO_REQUIRE(dw_mode >= 0 && dw_mode <= 2, "pico_rmsnorm_bwd_acc: dw_mode %d not in 0..2", dw_mode);
   PICO_REQUIRE(rows > 0 && cols > 0 && cols % 8 == 0, "pico_rmsnorm_bwd: bad shape rows=%lld cols=%lld",
                (long long)rows, (long long)cols);
   const int mc = maxc_for(cols);
@@ -276,8 +293,15 @@ int pico_rmsnorm_bwd(const void* dy, const void* dresidual, const void* x, const
   }
   if (rc) return rc;
 
-  PICO_LAUNCH(PICO_K_RMSNORM_DW, "rmsnorm_dw", s,
-              rmsnorm_dw_kernel<<<pico_cdiv(cols, 32), 256, 0, s>>>(part, (bf16_t*)dweight, nb, c));
+  const int g = pico_cdiv(cols, 32);
+  if (dw_mode == 0) {
+    PICO_LAUNCH(PICO_K_RMSNORM_DW, "rmsnorm_dw", s, rmsnorm_dw_kernel<0><<<g, 256, 0, s>>>(part, dweight, nb, c, 1.f));
+  } else if (dw_mode == 1) {
+    PICO_LAUNCH(PICO_K_RMSNORM_DW, "rmsnorm_dw", s, rmsnorm_dw_kernel<1><<<g, 256, 0, s>>>(part, dweight, nb, c, 1.f));
+  } else {
+    PICO_LAUNCH(PICO_K_RMSNORM_DW, "rmsnorm_dw", s,
+                rmsnorm_dw_kernel<2><<<g, 256, 0, s>>>(part, dweight, nb, c, dw_scale));
+  }
   return 0;
 }
 

@@ -61,6 +61,7 @@ class _RMSNormFn(torch.autograd.Function):
                                         _lib.ptr(rstd), rows, cols, float(eps), _lib.stream_of(x)), "pico_rmsnorm_fwd")
         x_eff = res_out if res_out is not None else x2
         ctx.save_for_backward(x_eff, w, rstd)
+        ctx.weight_param = weight if weight.requires_grad else None
         ctx.shape = shape
         ctx.has_residual = residual is not None
         ctx.prenorm = prenorm
@@ -80,13 +81,35 @@ class _RMSNormFn(torch.autograd.Function):
             dres = rest[0].reshape(-1, cols).contiguous()
         lib = _lib.load()
         dx = torch.empty_like(x_eff)
-        dw = torch.empty_like(w)
+        mode, target, scale, ready = _norm_grad_target(ctx.weight_param, w)
+        dw = target if mode == 0 else None
         ws = torch.empty(lib.pico_rmsnorm_bwd_workspace_bytes(rows, cols), dtype=torch.uint8, device=dy.device)
-        _lib.check(lib.pico_rmsnorm_bwd(_lib.ptr(dy2), _lib.ptr(dres), _lib.ptr(x_eff), _lib.ptr(w), _lib.ptr(rstd),
-                                        _lib.ptr(dx), _lib.ptr(dw), _lib.ptr(ws), rows, cols, _lib.stream_of(dy)),
-                   "pico_rmsnorm_bwd")
+        _lib.check(lib.pico_rmsnorm_bwd_acc(_lib.ptr(dy2), _lib.ptr(dres), _lib.ptr(x_eff), _lib.ptr(w),
+                                            _lib.ptr(rstd), _lib.ptr(dx), _lib.ptr(target), mode, float(scale),
+                                            _lib.ptr(ws), rows, cols, _lib.stream_of(dy)), "pico_rmsnorm_bwd")
+        if ready is not None:
+            ready()
         dx = dx.view(ctx.shape)
         return dx, (dx if ctx.has_residual else None), dw, None, None
+
+
+def _norm_grad_target(p, w):
+    """Where the norm-weight gradient goes (the micro-batch accumulation folded into the dw reduction,
+    as wgrad_accumulate does for the projections): (dw_mode, buffer, scale, ready-callback).
+    mode 2: DataParallelBucket's fp32 main_grad += dw (x 1/W on the syncing micro-batch), then the
+    bucket is told the parameter is ready; mode 1: bf16 .grad += dw in place (no DP wrapper, no hooks);
+    mode 0: a fresh dw handed to autograd (first micro-batch, hooks, fusion disabled)."""
+    if p is not None and wgrad_fusion_enabled() and p.is_contiguous():
+        mg = getattr(p, "main_grad", None)
+        if mg is not None and getattr(p, "_pico_wgrad_ready", None) is not None:
+            if mg.dtype == torch.float32 and mg.is_contiguous() and mg.shape == p.shape:
+                sync, world = p._pico_wgrad_sync()
+                return 2, mg, (1.0 / world if sync else 1.0), p._pico_wgrad_ready
+        elif mg is None and not _has_hooks(p):
+            g = p.grad
+            if g is not None and g.dtype == p.dtype and g.is_contiguous() and g.shape == p.shape:
+                return 1, g, 1.0, None
+    return 0, torch.empty_like(w), 1.0, None
 
 
 def rms_norm(x, weight, eps=1e-5, residual=None, prenorm=False):

@@ -86,6 +86,49 @@ def test_rmsnorm_residual_prenorm():
     assert torch.equal(x.grad, r.grad)
 
 
+def test_rmsnorm_dw_accumulate_modes():
+    """pico_rmsnorm_bwd_acc: mode 2 (fp32 (g + dw) * scale) with g = 0, scale = 1 gives the fp32 dw sum;
+    mode 1 == bf16(g_bf16 + that sum) and mode 2 == (g + sum) * scale bit for bit; dx identical in every
+    mode; mode 0 == pico_rmsnorm_bwd."""
+    import ctypes  # noqa: F401
+    from picotron_amd import _lib as L
+    torch.manual_seed(3)
+    rows, cols = 300, 2048
+    x = torch.randn(rows, cols, dtype=BF, device=DEV)
+    w = (1 + 0.1 * torch.randn(cols, device=DEV)).to(BF)
+    dy = torch.randn(rows, cols, dtype=BF, device=DEV)
+    rstd = torch.rsqrt(x.float().pow(2).mean(1) + 1e-5)
+    lib = L.load()
+    ws = torch.empty(lib.pico_rmsnorm_bwd_workspace_bytes(rows, cols), dtype=torch.uint8, device=DEV)
+
+    def run(mode, target, scale=1.0):
+        dx = torch.empty_like(x)
+        L.check(lib.pico_rmsnorm_bwd_acc(L.ptr(dy), None, L.ptr(x), L.ptr(w), L.ptr(rstd), L.ptr(dx), L.ptr(target),
+                                         mode, scale, L.ptr(ws), rows, cols, L.stream_of(x)), "bwd_acc")
+        torch.cuda.synchronize()
+        return dx
+    s32 = torch.zeros(cols, device=DEV)
+    dx2 = run(2, s32)
+    g1 = torch.randn(cols, device=DEV).to(BF)
+    exp1 = (g1.float() + s32).to(BF)
+    dx1 = run(1, g1)
+    assert torch.equal(g1, exp1)
+    g2 = torch.randn(cols, device=DEV)
+    exp2 = (g2 + s32) * 0.25
+    run(2, g2, 0.25)
+    assert torch.equal(g2, exp2)
+    d0 = torch.empty(cols, dtype=BF, device=DEV)
+    dx0 = run(0, d0)
+    assert torch.equal(d0, s32.to(BF))
+    assert torch.equal(dx0, dx1) and torch.equal(dx0, dx2)
+    d_ref = torch.empty(cols, dtype=BF, device=DEV)
+    dxr = torch.empty_like(x)
+    L.check(lib.pico_rmsnorm_bwd(L.ptr(dy), None, L.ptr(x), L.ptr(w), L.ptr(rstd), L.ptr(dxr), L.ptr(d_ref),
+                                 L.ptr(ws), rows, cols, L.stream_of(x)), "bwd")
+    torch.cuda.synchronize()
+    assert torch.equal(d_ref, d0) and torch.equal(dxr, dx0)
+
+
 def test_rmsnorm_rejects_cpu_tensors():
     ops = _ops()
     with pytest.raises(RuntimeError):
