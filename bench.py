@@ -33,6 +33,23 @@ HBM_PEAK_GBS = 8000.0
 BF16_PEAK_TFLOPS = 256 * 4096 * 2.4e9 / 1e12  # 2516.6 dense
 
 
+def pmc_traffic(kernel_name):
+    """HBM bytes per launch of `kernel_name` from the newest committed PMC summary
+    (profiles/r*_pmc_attn_c2.json: scripts/pmc_attn.sh + scripts/pmc_summary.py --json on the attention
+    micro-bench at this bench's shapes; 2 x FETCH_SIZE (gfx950 half-count correction) + WRITE_SIZE,
+    MI355X_MICROARCH.md §HBM). (None, None) when no summary covers the kernel."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_attn_c2.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as fh:
+        recs = json.load(fh)
+    for k, rec in recs.items():
+        if k.startswith(kernel_name + "_kernel<") and "traffic_bytes" in rec:
+            return round(rec["traffic_bytes"]), os.path.relpath(files[-1], ROOT) + ": " + k
+    return None, None
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -46,6 +63,8 @@ def kernel_work(kid, cfg, mbs, seq):
     Hkv = cfg.num_key_value_heads
     D = Hd // H
     attn_fwd = 4.0 * mbs * H * seq * seq * D / 2  # causal
+    nkb = -(-seq // 256)  # 256-key blocks of the backward
+    dq_slabs = sum(min(nkb, q // 256 + 1) for q in range(seq)) / seq  # causal: mean slabs per query row
     table = {
         L.K_ATTN_FWD: (attn_fwd, "flop", "mfma"),
         L.K_ATTN_BWD: (2.5 * attn_fwd, "flop", "mfma"),
@@ -56,8 +75,10 @@ def kernel_work(kid, cfg, mbs, seq):
         L.K_ROPE: (2 * T * (H + Hkv) * D * 2, "byte", "hbm"),  # q|k heads in one launch, read + write
         L.K_SWIGLU_FWD: (3 * T * I * 2, "byte", "hbm"),
         L.K_SWIGLU_BWD: (5 * T * I * 2, "byte", "hbm"),
-        L.K_ATTN_BWD_PRE: (2 * T * Hd * 2 + T * H * 4 + T * Hd * 4, "byte", "hbm"),
-        L.K_ATTN_BWD_DQ: (T * Hd * 4 + T * Hd * 2, "byte", "hbm"),
+        # reads O, dO, LSE; writes delta and LSE*log2(e) (fp32 per query row and head)
+        L.K_ATTN_BWD_PRE: (2 * T * Hd * 2 + 3 * T * H * 4, "byte", "hbm"),
+        # reads the fp32 dQ partial slabs of the key blocks at or before each query row, writes bf16 dQ
+        L.K_ATTN_BWD_DQ: (dq_slabs * T * Hd * 4 + T * Hd * 2, "byte", "hbm"),
     }
     return table.get(kid)
 
@@ -200,8 +221,9 @@ def main():
             achieved, peak, u = amount / avg_s / 1e12, BF16_PEAK_TFLOPS, "TFLOP/s"
         else:
             achieved, peak, u = amount / avg_s / 1e9, HBM_PEAK_GBS, "GB/s"
+        traffic, traffic_src = pmc_traffic(dom)
         roofline = {"kernel": dom, "bound": bound, "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": u,
-                    "frac": round(achieved / peak, 4), "traffic": None,
+                    "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_source": traffic_src,
                     "work_per_launch": amount, "avg_launch_us": round(kernels[dom]["avg_us"], 2),
                     "timed_over": ("the timed region" if kernel_timing_live else
                                    "one eager step right after the timed region (graph replays carry no per-launch events)")}
