@@ -43,13 +43,15 @@
 
 namespace {
 
-constexpr int BK = 256;  // keys per workgroup
+constexpr int BK = 256;  // keys per workgroup (128 with two workgroups per CU measured slower: 93 -> 100 us)
 constexpr int STAMP_TILES = 40, STAMP_PH = 6;
 constexpr int64_t STAMP_BYTES = PICO_BWD_STAMP ? 8 * STAMP_TILES * STAMP_PH * 8 : 0;
 constexpr int BQ = 32;   // query rows per tile
 
 template <int D>
 struct BwdCfg {
+  static constexpr int NW = BK / 32;  // waves (32 keys each)
+  static constexpr int NTH = NW * 64;
   static constexpr int KS = D / 16, DT = D / 32, CPR = D / 8;
   static constexpr int RB = D * 2;              // bytes per Q/dO/K image row
   static constexpr int QIMG = BQ * RB;          // one Q (or dO) tile image
@@ -63,7 +65,7 @@ struct BwdCfg {
   static constexpr int RPP = 1024 / RB;         // image rows per 1-KiB DMA piece
   static constexpr int NQP = QIMG / 1024;       // pieces per Q (or dO) tile
   static constexpr int NP = 2 * NQP + 1;        // pieces per tile
-  static constexpr int NPW = (NP + 7) / 8;      // max pieces per wave
+  static constexpr int NPW = (NP + NW - 1) / NW;  // max pieces per wave
 };
 
 // One LDS-DMA piece (16 B per lane, lane-linear at the wave-uniform LDS byte address lds_base) issued
@@ -150,8 +152,8 @@ PICO_DEV bf16x8 kimg_read_tr16(const char* base, int row0, int col0, int lane) {
   return __builtin_bit_cast(bf16x8, v);
 }
 
-// delta[bh, q] = sum_d dO * O, lse2[bh, q] = LSE * log2(e); rows q in [Sq, Sq_pad) get delta = 0 and
-// lse2 = +inf. Rows are ordered (b, h, q) so the LSE reads and the delta / lse2 writes are contiguous;
+// delta[bh, q] = -sum_d dO * O (negated), lse2[bh, q] = LSE * log2(e); rows q in [Sq, Sq_pad) get
+// delta = 0 and lse2 = +inf. Rows are ordered (b, h, q) so the LSE reads and the delta / lse2 writes are contiguous;
 // each row of O / dO is one contiguous 2D-byte segment read by D/8 lanes.
 template <int D>
 __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(const pico_attn_args a, float* __restrict__ delta,
@@ -182,7 +184,7 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(const pico_attn_args 
 #pragma unroll
   for (int o = LPR / 2; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
   if (sub == 0) {
-    delta[row] = s;
+    delta[row] = -s;  // negated: it initialises the dP accumulator (dP - delta in the MFMA chain)
     lse2[row] = a.lse[bh * a.seqlen_q + q] * LOG2E;
   }
 }
@@ -191,12 +193,12 @@ template <int D>
 constexpr int bwd_waves_per_eu() { return D == 64 ? PICO_BWD_WAVES_PER_EU_D64 : 1; }
 
 template <int D, bool CAUSAL>
-__global__ __launch_bounds__(512, bwd_waves_per_eu<D>()) void attn_bwd_kernel(
+__global__ __launch_bounds__(BwdCfg<D>::NTH, bwd_waves_per_eu<D>()) void attn_bwd_kernel(
     const pico_attn_args a, float scale, float scale_log2, const float* __restrict__ delta_g,
     const float* __restrict__ lse2_g, int sq_pad, float* __restrict__ dq_part, int64_t slab,
     float* __restrict__ trash) {
   using C = BwdCfg<D>;
-  constexpr int KS = C::KS, DT = C::DT, CPR = C::CPR;
+  constexpr int KS = C::KS, DT = C::DT, CPR = C::CPR, NW = C::NW;
   __shared__ __attribute__((aligned(16))) char smem[C::SMEM];
   char* kimg = smem;
   char* ring = smem + C::KIMG;
@@ -236,15 +238,15 @@ __global__ __launch_bounds__(512, bwd_waves_per_eu<D>()) void attn_bwd_kernel(
   const int nqt = Sq > qstart ? (Sq - qstart + BQ - 1) / BQ : 0;
   const int ntiles = G * nqt;
 
-  // ---- tile DMA: piece j is issued by wave j % 8 ----
+  // ---- tile DMA: piece j is issued by wave j % NW ----
   //  j < NQP: Q rows RPP*j + lane / CPR, LDS chunk lane % CPR  <- source chunk (lane % CPR) ^ swz(row)
   //  j < 2 NQP: the same for dO;  j == 2 NQP: lanes 0-7 LSE*log2e[q0 .. q0+31], 8-15 delta (16..63 repeat)
-  const int my_np = (C::NP / 8) + (wave < C::NP % 8 ? 1 : 0);  // wave-uniform piece count
+  const int my_np = (C::NP / NW) + (wave < C::NP % NW ? 1 : 0);  // wave-uniform piece count
   int pc_row[C::NPW], pc_col[C::NPW], pc_kind[C::NPW];
   unsigned pc_dst[C::NPW];
 #pragma unroll
   for (int i = 0; i < C::NPW; ++i) {
-    const int j = wave + 8 * i;
+    const int j = wave + NW * i;
     if (j < 2 * C::NQP) {
       const int jj = j % C::NQP, row = C::RPP * jj + lane / CPR;
       pc_kind[i] = j < C::NQP ? 0 : 1;
@@ -310,7 +312,7 @@ __global__ __launch_bounds__(512, bwd_waves_per_eu<D>()) void attn_bwd_kernel(
   }
 
   // ---- K block -> LDS image; V fragments -> registers (B operand of dP = dO V^T) ----
-  for (int id = threadIdx.x; id < BK * CPR; id += 512) {
+  for (int id = threadIdx.x; id < BK * CPR; id += C::NTH) {
     const int row = id / CPR, ch = id % CPR;
     const int key = k0 + row;
     const u16x8 v = *reinterpret_cast<const u16x8*>(kg + (int64_t)min(key, Sk - 1) * a.k_strides[1] + ch * 8);
@@ -341,11 +343,19 @@ __global__ __launch_bounds__(512, bwd_waves_per_eu<D>()) void attn_bwd_kernel(
   auto active = [&](int q0) __attribute__((always_inline)) { return !CAUSAL || kw <= q0 + BQ - 1; };
 
   // S[q][key] and dP[q][key] of tile t: A = Q / dO rows (LDS), B = K^T (LDS) / V^T (registers)
+  // dP's accumulator starts at -delta of its rows (the tile's LSE/delta piece), so the chain yields
+  // dP - delta directly
   auto sdp = [&](int si, f32x16& s, f32x16& dp) __attribute__((always_inline)) {
     const char* qs = slot_of(si);
     const char* dos = qs + C::QIMG;
+    const float* nd = (const float*)(qs + 2 * C::QIMG) + 32;  // -delta[32]
     s = (f32x16)0.f;
-    dp = (f32x16)0.f;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(nd + 8 * g + 4 * h);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) dp[4 * g + j] = v[j];
+    }
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       const bf16x8 qa = lds_read_b128(qs, lds_off<D>(r, 2 * ks + h));
@@ -356,19 +366,17 @@ __global__ __launch_bounds__(512, bwd_waves_per_eu<D>()) void attn_bwd_kernel(
     }
   };
 
-  // P = exp2(S * scale*log2e - LSE*log2e) (in s), dS = P * (dP - delta) (in dp); then
-  // dV[key][d] += P^T dO, dK[key][d] += dS^T Q (k index = the tile's query rows)
-  auto softmax_dkdv = [&](int si, int q0, f32x16& s, f32x16& dp) __attribute__((always_inline)) {
+  // P = exp2(S * scale*log2e - LSE*log2e) (in s), dS = P * (dP - delta) (dp holds dP - delta); then
+  // dV[key][d] += P^T dO, dK[key][d] += dS^T Q (k index = the tile's query rows). sf receives dS in
+  // bf16 (the dK operand), reused for the dS^T image.
+  auto softmax_dkdv = [&](int si, int q0, f32x16& s, const f32x16& dp, bf16x8 (&sf)[2]) __attribute__((always_inline)) {
     const char* qs = slot_of(si);
     const char* dos = qs + C::QIMG;
     const float* lsd = (const float*)(qs + 2 * C::QIMG);
     // rows of this lane's accumulator registers: q = 8g + 4h + (0..3), g = 0..3
-    f32x4 l2[4], dl[4];
+    f32x4 l2[4];
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      l2[g] = *reinterpret_cast<const f32x4*>(lsd + 8 * g + 4 * h);
-      dl[g] = *reinterpret_cast<const f32x4*>(lsd + 32 + 8 * g + 4 * h);
-    }
+    for (int g = 0; g < 4; ++g) l2[g] = *reinterpret_cast<const f32x4*>(lsd + 8 * g + 4 * h);
 #pragma unroll
     for (int i = 0; i < 16; ++i) s[i] = fast_exp2(__builtin_fmaf(s[i], scale_log2, -l2[i >> 2][i & 3]));
     if ((CAUSAL && kw + 31 > q0) || (k0 + BK > Sk)) {  // wave-uniform
@@ -379,37 +387,36 @@ __global__ __launch_bounds__(512, bwd_waves_per_eu<D>()) void attn_bwd_kernel(
       for (int i = 0; i < 16; ++i) s[i] = ((i & 3) + 8 * (i >> 2) < rel || kill_all) ? 0.f : s[i];
     }
 #pragma unroll
-    for (int i = 0; i < 16; ++i) dp[i] = s[i] * (dp[i] - dl[i >> 2][i & 3]);
-#pragma unroll
     for (int st = 0; st < 2; ++st) {
       float pv[8], sv[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         pv[j] = s[8 * st + j];
-        sv[j] = dp[8 * st + j];
+        sv[j] = s[8 * st + j] * dp[8 * st + j];
       }
       const bf16x8 pf = pack_frag(pv);
-      const bf16x8 sf = pack_frag(sv);
+      sf[st] = pack_frag(sv);
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
         const bf16x8 dof = lds_read_tr32<D>(dos, 16 * st, 32 * dt, lane);
         dv[dt] = mfma32(pf, dof, dv[dt]);
         const bf16x8 qf = lds_read_tr32<D>(qs, 16 * st, 32 * dt, lane);
-        dk[dt] = mfma32(sf, qf, dk[dt]);
+        dk[dt] = mfma32(sf[st], qf, dk[dt]);
       }
     }
   };
 
-  // dS^T image [key][q] (bf16) of tile t: registers 4g..4g+3 are q = 8g + 4h + 0..3 -> one 8-B store each
-  auto ds_write = [&](int par, const f32x16& dp) __attribute__((always_inline)) {
+  // dS^T image [key][q] (bf16) of tile t: elements 4g..4g+3 (sf[g / 2] half g % 2) are q = 8g + 4h + 0..3
+  // -> one 8-B store each
+  auto ds_write = [&](int par, const bf16x8 (&sf)[2]) __attribute__((always_inline)) {
     char* dsimg = dsimg0 + (unsigned)par * (unsigned)C::DSIMG;
     const int krow = 32 * wave + r;
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-      u16x4 w;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) w[j] = f2bf(dp[4 * g + j]);
-      *reinterpret_cast<u16x4*>(dsimg + ds_img_off(krow, 8 * g + 4 * h)) = w;
+      typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+      const bf16x8 v = sf[g >> 1];
+      const bf16x4 w = (g & 1) ? bf16x4{v[4], v[5], v[6], v[7]} : bf16x4{v[0], v[1], v[2], v[3]};
+      *reinterpret_cast<bf16x4*>(dsimg + ds_img_off(krow, 8 * g + 4 * h)) = w;
     }
   };
 
@@ -426,8 +433,8 @@ __global__ __launch_bounds__(512, bwd_waves_per_eu<D>()) void attn_bwd_kernel(
     const int g16 = lane >> 4, i16 = lane & 15;
     typedef __attribute__((ext_vector_type(8))) short i16x8;
 #pragma unroll
-    for (int tt = 0; tt < NT / 8; ++tt) {
-      const int tl = wave + 8 * tt;
+    for (int tt = 0; tt < NT / NW; ++tt) {
+      const int tl = wave + NW * tt;
       const int qi = tl / (D / 16), di = tl % (D / 16);
       const int qc = 16 * qi + 4 * (i16 & 3);
       // A = dS[q = 16 qi + (lane & 15)][key = kk + 8 g16 + j]: transposed read of the [key][q] image
@@ -459,12 +466,15 @@ __global__ __launch_bounds__(512, bwd_waves_per_eu<D>()) void attn_bwd_kernel(
       }
       // every lane stores (rows past Sq go to a trash slot), so the per-tile count of vector-memory
       // instructions is fixed and the ring's vmcnt waits stay exact
-      float* dst = dq_part + kb * slab + (int64_t)b * Sq * Hq * D + c.hq * D + di * 16 + i16;
+      const int qr = c.q0 + qi * 16 + 4 * g16;  // this lane's first row
+      float* dst = dq_part + kb * slab + ((int64_t)b * Sq + qr) * Hq * D + c.hq * D + di * 16 + i16;
+      const int rs = Hq * D;  // row stride (elements)
+      if (c.q0 + BQ <= Sq) {  // wave-uniform: whole tile in range
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int q = c.q0 + qi * 16 + 4 * g16 + j;
-        float* p = q < Sq ? dst + (int64_t)q * Hq * D : trash + lane;
-        *p = acc[j] * scale;
+        for (int j = 0; j < 4; ++j) dst[j * rs] = acc[j] * scale;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) *(qr + j < Sq ? dst + j * rs : trash + lane) = acc[j] * scale;
       }
     }
   };
@@ -476,8 +486,8 @@ __global__ __launch_bounds__(512, bwd_waves_per_eu<D>()) void attn_bwd_kernel(
   // Per-wave vector-memory ops in issue order, iteration j: DMA pieces of tile j+PD, dQ stores of j-1.
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();  // K image and the prologue tiles visible
-  constexpr int NST = 4 * ((BQ / 16) * (D / 16) / 8);  // dQ stores per wave per tile
-  const bool dq_first = PICO_BWD_STAGGER && D == 64 && wave >= 4;  // D = 128: no registers to spare
+  constexpr int NST = 4 * ((BQ / 16) * (D / 16) / NW);  // dQ stores per wave per tile
+  const bool dq_first = PICO_BWD_STAGGER && D == 64 && wave >= NW / 2;  // D = 128: no registers to spare
   Tc cur = {hk * G, qstart}, prev = cur;
   int si_cur = 0, si_nxt = C::PD;  // ring slots of tiles t and t + PD
   for (int t = 0; t < ntiles; ++t) {
@@ -498,10 +508,11 @@ __global__ __launch_bounds__(512, bwd_waves_per_eu<D>()) void attn_bwd_kernel(
     stamp(t, 2);
     if (active(cur.q0)) {
       f32x16 s, dp;
+      bf16x8 sf[2];
       sdp(si_cur, s, dp);
-      softmax_dkdv(si_cur, cur.q0, s, dp);
+      softmax_dkdv(si_cur, cur.q0, s, dp, sf);
       stamp(t, 3);
-      ds_write(t & 1, dp);
+      ds_write(t & 1, sf);
     }
     stamp(t, 4);
     if (!dq_first && t >= 1) dq_tile((t - 1) & 1, prev);
@@ -606,11 +617,11 @@ int launch_bwd(const pico_attn_args* a, hipStream_t s) {
   if (nblk > 0) {
     if (a->causal) {
       PICO_LAUNCH(PICO_K_ATTN_BWD, "attn_bwd", s,
-                  attn_bwd_kernel<D, true><<<(int)nblk, 512, 0, s>>>(*a, a->softmax_scale, sl2, delta, lse2, sq_pad,
+                  attn_bwd_kernel<D, true><<<(int)nblk, BwdCfg<D>::NTH, 0, s>>>(*a, a->softmax_scale, sl2, delta, lse2, sq_pad,
                                                                      dq_part, slab, trash));
     } else {
       PICO_LAUNCH(PICO_K_ATTN_BWD, "attn_bwd", s,
-                  attn_bwd_kernel<D, false><<<(int)nblk, 512, 0, s>>>(*a, a->softmax_scale, sl2, delta, lse2, sq_pad,
+                  attn_bwd_kernel<D, false><<<(int)nblk, BwdCfg<D>::NTH, 0, s>>>(*a, a->softmax_scale, sl2, delta, lse2, sq_pad,
                                                                       dq_part, slab, trash));
     }
   }
