@@ -66,7 +66,8 @@ enum {
   PICO_K_CE_FWD = 16,
   PICO_K_CE_BWD = 17,
   PICO_K_TRANSPOSE = 18,
-  PICO_K_COUNT = 19
+  PICO_K_ATTN_BWD_DKV = 19,
+  PICO_K_COUNT = 20
 };
 
 int pico_abi_version(void);

@@ -196,7 +196,7 @@ template <int D, bool CAUSAL>
 __global__ __launch_bounds__(BwdCfg<D>::NTH, bwd_waves_per_eu<D>()) void attn_bwd_kernel(
     const pico_attn_args a, float scale, float scale_log2, const float* __restrict__ delta_g,
     const float* __restrict__ lse2_g, int sq_pad, float* __restrict__ dq_part, int64_t slab,
-    float* __restrict__ trash) {
+    float* __restrict__ trash, int hsplit, float* __restrict__ dkv_part) {
   using C = BwdCfg<D>;
   constexpr int KS = C::KS, DT = C::DT, CPR = C::CPR, NW = C::NW;
   __shared__ __attribute__((aligned(16))) char smem[C::SMEM];
@@ -221,9 +221,14 @@ __global__ __launch_bounds__(BwdCfg<D>::NTH, bwd_waves_per_eu<D>()) void attn_bw
   const int G = (int)(a.heads_q / a.heads_kv);
 
   // heaviest key blocks first (causal: block 0 sees every query)
-  const int nbh = (int)(a.batch * a.heads_kv);
+  // Small grids (GQA, few heads, short sequences): the (query head, query tile) list of a key block may
+  // be split over `hsplit` workgroups (hs) so the grid fills the chip; each then writes fp32 dK/dV
+  // partials that attn_bwd_dkv_kernel sums
+  const int nbh = (int)(a.batch * a.heads_kv) * hsplit;
   const int kb = blockIdx.x / nbh;
-  const int bh = blockIdx.x % nbh;
+  const int bhs = blockIdx.x % nbh;
+  const int hs = bhs % hsplit;
+  const int bh = bhs / hsplit;
   const int b = bh / (int)a.heads_kv;
   const int hk = bh % (int)a.heads_kv;
 
@@ -236,7 +241,10 @@ __global__ __launch_bounds__(BwdCfg<D>::NTH, bwd_waves_per_eu<D>()) void attn_bw
 
   const int qstart = CAUSAL ? k0 : 0;  // k0 is a multiple of BQ
   const int nqt = Sq > qstart ? (Sq - qstart + BQ - 1) / BQ : 0;
-  const int ntiles = G * nqt;
+  const int ntot = G * nqt;  // tiles of this key block: (query head of the group, query tile)
+  const int tb = (int)((int64_t)ntot * hs / hsplit);
+  const int ntiles = (int)((int64_t)ntot * (hs + 1) / hsplit) - tb;
+  const int hq0 = hk * G + tb / nqt, q00 = qstart + (tb % nqt) * BQ;  // first tile of this workgroup
 
   // ---- tile DMA: piece j is issued by wave j % NW ----
   //  j < NQP: Q rows RPP*j + lane / CPR, LDS chunk lane % CPR  <- source chunk (lane % CPR) ^ swz(row)
@@ -304,7 +312,7 @@ __global__ __launch_bounds__(BwdCfg<D>::NTH, bwd_waves_per_eu<D>()) void attn_bw
     }
   };
   // the first PD tiles go out before the K/V prologue loads; nxt = coordinates of tile PD afterwards
-  Tc nxt = {hk * G, qstart};
+  Tc nxt = {hq0, q00};
 #pragma unroll
   for (int j = 0; j < C::PD; ++j) {
     if (j < ntiles) issue(j, nxt);
@@ -488,7 +496,7 @@ __global__ __launch_bounds__(BwdCfg<D>::NTH, bwd_waves_per_eu<D>()) void attn_bw
   __syncthreads();  // K image and the prologue tiles visible
   constexpr int NST = 4 * ((BQ / 16) * (D / 16) / NW);  // dQ stores per wave per tile
   const bool dq_first = PICO_BWD_STAGGER && D == 64 && wave >= NW / 2;  // D = 128: no registers to spare
-  Tc cur = {hk * G, qstart}, prev = cur;
+  Tc cur = {hq0, q00}, prev = cur;
   int si_cur = 0, si_nxt = C::PD;  // ring slots of tiles t and t + PD
   for (int t = 0; t < ntiles; ++t) {
     stamp(t, 0);
@@ -534,16 +542,33 @@ __global__ __launch_bounds__(BwdCfg<D>::NTH, bwd_waves_per_eu<D>()) void attn_bw
   }
 #endif
   // ---- epilogue: dK = scale * acc, dV = acc; lane holds d = 32 dt + r, keys kw + acc_row(i, h) ----
-  bf16_t* dkg = (bf16_t*)a.dk + b * a.dk_strides[0] + hk * a.dk_strides[2];
-  bf16_t* dvg = (bf16_t*)a.dv + b * a.dv_strides[0] + hk * a.dv_strides[2];
+  if (hsplit == 1) {
+    bf16_t* dkg = (bf16_t*)a.dk + b * a.dk_strides[0] + hk * a.dk_strides[2];
+    bf16_t* dvg = (bf16_t*)a.dv + b * a.dv_strides[0] + hk * a.dv_strides[2];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int key = kw + acc_row(i, h);
-    if (key < Sk) {
+    for (int i = 0; i < 16; ++i) {
+      const int key = kw + acc_row(i, h);
+      if (key < Sk) {
 #pragma unroll
-      for (int dt = 0; dt < DT; ++dt) {
-        dkg[(int64_t)key * a.dk_strides[1] + 32 * dt + r] = f2bf(dk[dt][i] * scale);
-        dvg[(int64_t)key * a.dv_strides[1] + 32 * dt + r] = f2bf(dv[dt][i]);
+        for (int dt = 0; dt < DT; ++dt) {
+          dkg[(int64_t)key * a.dk_strides[1] + 32 * dt + r] = f2bf(dk[dt][i] * scale);
+          dvg[(int64_t)key * a.dv_strides[1] + 32 * dt + r] = f2bf(dv[dt][i]);
+        }
+      }
+    }
+  } else {  // fp32 partials [hs][dK | dV][b][key][hk][D]
+    const int64_t part = (int64_t)a.batch * Sk * a.heads_kv * D;
+    float* pk = dkv_part + (int64_t)(2 * hs) * part + ((int64_t)b * Sk * a.heads_kv + hk) * D;
+    float* pv = pk + part;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int key = kw + acc_row(i, h);
+      if (key < Sk) {
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+          pk[(int64_t)key * a.heads_kv * D + 32 * dt + r] = dk[dt][i] * scale;
+          pv[(int64_t)key * a.heads_kv * D + 32 * dt + r] = dv[dt][i];
+        }
       }
     }
   }
@@ -589,6 +614,51 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const pico_attn_args a
                             sub * 8) = o;
 }
 
+// dK / dV [b, key, hk, :] = sum over the hsplit workgroups' fp32 partials (fixed order) -> bf16 (strided)
+template <int D>
+__global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const pico_attn_args a, const float* __restrict__ dkv_part,
+                                                           int hsplit) {
+  constexpr int LPR = D / 8;
+  const int64_t part = a.batch * a.seqlen_k * a.heads_kv * D;
+  const int64_t rows = a.batch * a.seqlen_k * a.heads_kv;
+  const int64_t row = ((int64_t)blockIdx.x * 256 + threadIdx.x) / LPR;
+  const int sub = threadIdx.x % LPR;
+  if (row >= rows) return;
+  const int hk = (int)(row % a.heads_kv);
+  const int64_t bk = row / a.heads_kv;
+  const int key = (int)(bk % a.seqlen_k);
+  const int b = (int)(bk / a.seqlen_k);
+  for (int which = 0; which < 2; ++which) {
+    f32x4 x0 = (f32x4)0.f, x1 = (f32x4)0.f;
+    for (int hs = 0; hs < hsplit; ++hs) {
+      const f32x4* src = reinterpret_cast<const f32x4*>(dkv_part + (2 * hs + which) * part + row * D + sub * 8);
+      x0 += src[0];
+      x1 += src[1];
+    }
+    u16x8 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      o[j] = f2bf(x0[j]);
+      o[4 + j] = f2bf(x1[j]);
+    }
+    bf16_t* dst = which ? (bf16_t*)a.dv + b * a.dv_strides[0] + key * a.dv_strides[1] + hk * a.dv_strides[2]
+                        : (bf16_t*)a.dk + b * a.dk_strides[0] + key * a.dk_strides[1] + hk * a.dk_strides[2];
+    *reinterpret_cast<u16x8*>(dst + sub * 8) = o;
+  }
+}
+
+// tile-list split of a key block (see attn_bwd_kernel): the smallest factor (<= 8) giving at least two
+// workgroups per CU (512 = one launch wave of 256 CUs x 2), at most the block's query tile count
+int hsplit_for(const pico_attn_args* a) {
+  if (a->heads_kv <= 0 || a->heads_q % a->heads_kv != 0) return 1;  // rejected by the argument checks
+  const int64_t nblk = ((a->seqlen_k + BK - 1) / BK) * a->batch * a->heads_kv;
+  const int64_t tiles = (a->heads_q / a->heads_kv) * ((a->seqlen_q + BQ - 1) / BQ);  // of key block 0
+  if (nblk <= 0) return 1;
+  int d = 1;
+  while (d < 8 && nblk * d < 512 && 2 * d <= tiles) d *= 2;
+  return d;
+}
+
 int sq_padded(const pico_attn_args* a) { return (int)((a->seqlen_q + BQ - 1) / BQ) * BQ; }
 
 // [lse2 | delta], each [B*Hq][Sq_pad] fp32, rounded up to 64 floats
@@ -612,17 +682,25 @@ int launch_bwd(const pico_attn_args* a, hipStream_t s) {
   PICO_LAUNCH(PICO_K_ATTN_BWD_PRE, "attn_bwd_pre", s,
               attn_bwd_pre_kernel<D><<<pre_blocks, 256, 0, s>>>(*a, delta, lse2, sq_pad));
   const int nkb = (int)((a->seqlen_k + BK - 1) / BK);
-  const int64_t nblk = (int64_t)nkb * a->batch * a->heads_kv;
+  const int hsplit = hsplit_for(a);
+  const int64_t nblk = (int64_t)nkb * a->batch * a->heads_kv * hsplit;
+  // fp32 dK/dV partials (hsplit > 1) after the trash slot and the diagnostic stamps
+  float* dkv_part = hsplit > 1 ? trash + 64 + STAMP_BYTES / 4 : nullptr;
   const float sl2 = a->softmax_scale * LOG2E;
   if (nblk > 0) {
     if (a->causal) {
       PICO_LAUNCH(PICO_K_ATTN_BWD, "attn_bwd", s,
-                  attn_bwd_kernel<D, true><<<(int)nblk, BwdCfg<D>::NTH, 0, s>>>(*a, a->softmax_scale, sl2, delta, lse2, sq_pad,
-                                                                     dq_part, slab, trash));
+                  attn_bwd_kernel<D, true><<<(int)nblk, BwdCfg<D>::NTH, 0, s>>>(
+                      *a, a->softmax_scale, sl2, delta, lse2, sq_pad, dq_part, slab, trash, hsplit, dkv_part));
     } else {
       PICO_LAUNCH(PICO_K_ATTN_BWD, "attn_bwd", s,
-                  attn_bwd_kernel<D, false><<<(int)nblk, BwdCfg<D>::NTH, 0, s>>>(*a, a->softmax_scale, sl2, delta, lse2, sq_pad,
-                                                                      dq_part, slab, trash));
+                  attn_bwd_kernel<D, false><<<(int)nblk, BwdCfg<D>::NTH, 0, s>>>(
+                      *a, a->softmax_scale, sl2, delta, lse2, sq_pad, dq_part, slab, trash, hsplit, dkv_part));
+    }
+    if (hsplit > 1) {
+      const int kv_blocks = pico_cdiv(a->batch * a->seqlen_k * a->heads_kv * (D / 8), 256);
+      PICO_LAUNCH(PICO_K_ATTN_BWD_DKV, "attn_bwd_dkv", s,
+                  attn_bwd_dkv_kernel<D><<<kv_blocks, 256, 0, s>>>(*a, dkv_part, hsplit));
     }
   }
   if (a->causal) {
@@ -665,7 +743,9 @@ int64_t pico_attn_bwd_workspace_bytes(const pico_attn_args* a) {
   // lse2, delta [B*Hq*Sq_pad] fp32 + one fp32 dQ partial slab [B, Sq, Hq, D] per 256-key block
   const int64_t nkb = (a->seqlen_k + BK - 1) / BK;
   // + 64 floats of trash for the dQ stores of padded query rows
-  return (2 * lsd_floats(a) + nkb * a->batch * a->seqlen_q * a->heads_q * a->head_dim + 64) * 4 + STAMP_BYTES;
+  const int hs = hsplit_for(a);
+  const int64_t dkv = hs > 1 ? 2 * hs * a->batch * a->seqlen_k * a->heads_kv * a->head_dim : 0;  // fp32 partials
+  return (2 * lsd_floats(a) + nkb * a->batch * a->seqlen_q * a->heads_q * a->head_dim + 64 + dkv) * 4 + STAMP_BYTES;
 }
 
 int pico_attn_bwd(const pico_attn_args* a, void* stream) {

@@ -44,7 +44,7 @@ def main():
             o, lse = ops.attention_block_fwd(q, k, v, sc, causal)
             ops.attention_block_bwd(do, q, k, v, o, lse, sc, causal)
         torch.cuda.synchronize()
-        ids = [L.K_ATTN_FWD, L.K_ATTN_BWD_PRE, L.K_ATTN_BWD, L.K_ATTN_BWD_DQ]
+        ids = [L.K_ATTN_FWD, L.K_ATTN_BWD_PRE, L.K_ATTN_BWD, L.K_ATTN_BWD_DQ, L.K_ATTN_BWD_DKV]
         for i in ids:
             L.prof_enable(i, args.iters + 4)
         for _ in range(args.iters):

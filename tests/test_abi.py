@@ -73,6 +73,14 @@ def test_workspace_sizes(lib):
     a.seqlen_q = a.seqlen_k = 1000
     pad = ((4 * 32 * 1024 + 63) // 64) * 64
     assert lib.pico_attn_bwd_workspace_bytes(ctypes.byref(a)) == 2 * pad * 4 + 4 * (4 * 1000 * 32 * 64 * 4) + 256
+    # GQA 32/8 at S 1024: 4 key blocks x B 4 x 8 kv heads = 128 workgroups -> query heads split 4 ways,
+    # + fp32 dK/dV partials [4][2][B, S, Hkv, D]
+    a.seqlen_q = a.seqlen_k = 1024
+    a.heads_kv = 8
+    assert lib.pico_attn_bwd_workspace_bytes(ctypes.byref(a)) == (2 * 4 * 32 * 1024 * 4 + 4 * (4 * 1024 * 32 * 64 * 4)
+                                                                  + 256 + 4 * 2 * 4 * 1024 * 8 * 64 * 4)
+    a.heads_kv = 32  # MHA: no split
+    assert lib.pico_attn_bwd_workspace_bytes(ctypes.byref(a)) == 2 * 4 * 32 * 1024 * 4 + 4 * (4 * 1024 * 32 * 64 * 4) + 256
 
 
 def test_ops_fail_loudly_without_hip_tensors(lib):

@@ -250,6 +250,33 @@ def test_attention_vs_oracle(B, Sq, Sk, Hq, Hkv, D, causal):
     assert rel_l2(dv.transpose(1, 2).cpu(), dV) < 1e-2
 
 
+@pytest.mark.parametrize("B,Hq,Hkv", [(8, 64, 8), (4, 32, 8)])
+def test_attention_gqa_head_split(B, Hq, Hkv):
+    """Small grids whose key blocks split their (query head, query tile) list over 2 or 4 workgroups (GQA 64/8 at B 8, 32/8 at B 4:
+    fp32 dK/dV partials + attn_bwd_dkv_kernel) vs an fp32 torch reference on the GPU, causal S = 1024."""
+    ops = _ops()
+    torch.manual_seed(B * Hq + Hkv)
+    S, D = 1024, 64
+    q = torch.randn(B, S, Hq, D, dtype=BF, device=DEV)
+    k = torch.randn(B, S, Hkv, D, dtype=BF, device=DEV)
+    v = torch.randn(B, S, Hkv, D, dtype=BF, device=DEV)
+    do = torch.randn(B, S, Hq, D, dtype=BF, device=DEV)
+    sc = 1.0 / math.sqrt(D)
+    o, lse = ops.attention_block_fwd(q, k, v, sc, True)
+    dq, dk, dv = ops.attention_block_bwd(do, q, k, v, o, lse, sc, True)
+    G = Hq // Hkv
+    qf, kf, vf, dof = [t.float().transpose(1, 2).requires_grad_(True) for t in (q, k, v, do)]
+    kr, vr = kf.repeat_interleave(G, 1), vf.repeat_interleave(G, 1)
+    s = (qf @ kr.transpose(-1, -2)) * sc
+    s = s.masked_fill(torch.triu(torch.ones(S, S, dtype=torch.bool, device=DEV), 1), float("-inf"))
+    out = torch.softmax(s, -1) @ vr
+    gq, gk, gv = torch.autograd.grad(out, (qf, kf, vf), dof.detach())
+    assert rel_l2(o.transpose(1, 2).float(), out.detach()) < 4e-3
+    assert rel_l2(dq.transpose(1, 2).float(), gq) < 1e-2
+    assert rel_l2(dk.transpose(1, 2).float(), gk) < 1e-2
+    assert rel_l2(dv.transpose(1, 2).float(), gv) < 1e-2
+
+
 def test_attention_dq_f32_accumulate():
     ops = _ops()
     torch.manual_seed(3)
