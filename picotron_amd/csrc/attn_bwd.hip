@@ -36,6 +36,11 @@
 #ifndef PICO_BWD_STAMP
 #define PICO_BWD_STAMP 0
 #endif
+//   PICO_BWD_SCHED: S/dP operand reads all issued before the MFMAs (sched_group_barrier) (1) or
+//     left to the scheduler (0)
+#ifndef PICO_BWD_SCHED
+#define PICO_BWD_SCHED 1
+#endif
 //   PICO_BWD_STAGGER: waves 4-7 run the dQ tile of t-1 BEFORE tile t's S/dP (1) or after (0)
 #ifndef PICO_BWD_STAGGER
 #define PICO_BWD_STAGGER 1
@@ -364,13 +369,30 @@ __global__ __launch_bounds__(BwdCfg<D>::NTH, bwd_waves_per_eu<D>()) void attn_bw
 #pragma unroll
       for (int j = 0; j < 4; ++j) dp[4 * g + j] = v[j];
     }
+    if constexpr (PICO_BWD_SCHED && D == 64) {  // D = 128: no registers for all 24 operands at once
+      bf16x8 qa[KS], kbf[KS], da[KS];
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      const bf16x8 qa = lds_read_b128(qs, lds_off<D>(r, 2 * ks + h));
-      const bf16x8 kbf = lds_read_b128(kimg, kimg_off<D>(32 * wave + r, 2 * ks + h));
-      s = mfma32(qa, kbf, s);
-      const bf16x8 da = lds_read_b128(dos, lds_off<D>(r, 2 * ks + h));
-      dp = mfma32(da, vf[ks], dp);
+      for (int ks = 0; ks < KS; ++ks) {
+        qa[ks] = lds_read_b128(qs, lds_off<D>(r, 2 * ks + h));
+        kbf[ks] = lds_read_b128(kimg, kimg_off<D>(32 * wave + r, 2 * ks + h));
+        da[ks] = lds_read_b128(dos, lds_off<D>(r, 2 * ks + h));
+      }
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        s = mfma32(qa[ks], kbf[ks], s);
+        dp = mfma32(da[ks], vf[ks], dp);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x100, 3 * KS, 0);  // all operand reads first,
+      __builtin_amdgcn_sched_group_barrier(0x008, 2 * KS, 0);  // then the S / dP MFMAs
+    } else {
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const bf16x8 qa = lds_read_b128(qs, lds_off<D>(r, 2 * ks + h));
+        const bf16x8 kbf = lds_read_b128(kimg, kimg_off<D>(32 * wave + r, 2 * ks + h));
+        s = mfma32(qa, kbf, s);
+        const bf16x8 da = lds_read_b128(dos, lds_off<D>(r, 2 * ks + h));
+        dp = mfma32(da, vf[ks], dp);
+      }
     }
   };
 

@@ -82,7 +82,8 @@ PICO_DEV float halves_sum(float x) {
 }
 
 template <int D, bool CAUSAL>
-__global__ __launch_bounds__(256, FwdCfg<D>::WAVES_PER_EU) void attn_fwd_kernel(const pico_attn_args a, float scale_log2) {
+__global__ __launch_bounds__(256, FwdCfg<D>::WAVES_PER_EU)
+__attribute__((amdgpu_waves_per_eu(FwdCfg<D>::WAVES_PER_EU, FwdCfg<D>::WAVES_PER_EU))) void attn_fwd_kernel(const pico_attn_args a, float scale_log2) {
   using C = FwdCfg<D>;
   constexpr bool EARLY_V = PICO_FWD_EARLY_V < 0 ? D == 128 : PICO_FWD_EARLY_V != 0;
   constexpr int KS = C::KS;  // k-steps of the S^T product
@@ -218,15 +219,20 @@ __global__ __launch_bounds__(256, FwdCfg<D>::WAVES_PER_EU) void attn_fwd_kernel(
   // One 64-key tile for this wave. MASK: apply key <= lim_lane (causal) and key < Sk.
   auto tile_body = [&](const char* kb, unsigned vaddr, int n0, bool mask) __attribute__((always_inline)) {
     f32x16 s[2];
+    // every K fragment of the tile requested before the first MFMA (one LDS latency per tile, not per step)
+    bf16x8 kf[2][KS];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) kf[kt][ks] = lds_read_b128(kb, ks * C::KIMG + kt * 32 * 32);
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
       s[kt] = (f32x16)0.f;
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        const bf16x8 kf = lds_read_b128(kb, ks * C::KIMG + kt * 32 * 32);
-        s[kt] = mfma32(kf, qf[ks], s[kt]);
-      }
+      for (int ks = 0; ks < KS; ++ks) s[kt] = mfma32(kf[kt][ks], qf[ks], s[kt]);
     }
+    __builtin_amdgcn_sched_group_barrier(0x100, 2 * KS, 0);  // the K reads first,
+    __builtin_amdgcn_sched_group_barrier(0x008, 2 * KS, 0);  // then the S MFMAs
     bf16x8 vf0[2][DT], vf1[2][DT];
     if constexpr (EARLY_V) {  // in flight during the softmax VALU below
       v_reads(vf0, vaddr, std::integral_constant<int, 0>{});
