@@ -55,6 +55,20 @@ void pico_prof_post(int kid, hipStream_t s);
     if (_rc) return _rc;                               \
   } while (0)
 
+// Sum over the 64 lanes of a wave, result in every lane, without LDS (ds_bpermute) round trips:
+// DPP within rows of 16 (quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror), then
+// v_permlane16_swap (row pairs) and v_permlane32_swap (halves).
+PICO_DEV float wave_sum_dpp(float v) {
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140, 0xF, 0xF, false));
+  const auto r16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(r16[0]) + __uint_as_float(r16[1]);
+  const auto r32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r32[0]) + __uint_as_float(r32[1]);
+}
+
 // Compile-time loop: f(std::integral_constant<int, I>{}) for I = 0 .. N-1.
 template <int N, int I = 0, class F>
 __host__ __device__ __forceinline__ void static_for(F&& f) {

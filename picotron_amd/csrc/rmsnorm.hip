@@ -16,11 +16,7 @@ namespace {
 
 constexpr int WAVES = 4;
 
-PICO_DEV float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
+PICO_DEV float wave_sum(float v) { return wave_sum_dpp(v); }
 
 PICO_DEV void load8(const bf16_t* p, float* f) {
   u16x8 v = *reinterpret_cast<const u16x8*>(p);
