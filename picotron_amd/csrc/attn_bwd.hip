@@ -356,6 +356,43 @@ __global__ __launch_bounds__(BwdCfg<D>::NTH, bwd_waves_per_eu<D>()) void attn_bw
   auto active = [&](int q0) __attribute__((always_inline)) { return !CAUSAL || kw <= q0 + BQ - 1; };
 
   // S[q][key] and dP[q][key] of tile t: A = Q / dO rows (LDS), B = K^T (LDS) / V^T (registers)
+  // Lane-constant LDS offsets of the per-tile operand reads (D = 64), computed once and pinned in
+  // registers: an empty asm makes them opaque, so the compiler keeps 16 registers instead of
+  // re-deriving the XOR swizzles (~100 VALU) every tile. Tile-dependent parts are slot bases and
+  // immediate row deltas (16 Q/dO rows = 2 KiB: the swizzles depend on row bits 0-3 only).
+  unsigned qo[KS], ko[KS], tro[DT][2], dso[4];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    qo[ks] = lds_off<D>(r, 2 * ks + h);
+    ko[ks] = kimg_off<D>(32 * wave + r, 2 * ks + h);
+  }
+  {
+    const int g = lane >> 4, i = lane & 15, hh = g >> 1, q = i >> 2, p = i & 3;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      const int col = 32 * dt + 16 * (g & 1) + 4 * p;
+      tro[dt][0] = lds_off<D>(4 * hh + q, col >> 3) + (col & 7) * 2;
+      tro[dt][1] = lds_off<D>(4 * hh + q + 8, col >> 3) + (col & 7) * 2;
+    }
+  }
+#pragma unroll
+  for (int g = 0; g < 4; ++g) dso[g] = ds_img_off(32 * wave + r, 8 * g + 4 * h);
+  if constexpr (D == 64) {
+#pragma unroll
+    for (int k = 0; k < KS; ++k) asm volatile("" : "+v"(qo[k]), "+v"(ko[k]));
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) asm volatile("" : "+v"(tro[dt][0]), "+v"(tro[dt][1]));
+#pragma unroll
+    for (int g = 0; g < 4; ++g) asm volatile("" : "+v"(dso[g]));
+  }
+  auto tr_pair = [](const char* base, unsigned lo_off, unsigned hi_off) __attribute__((always_inline)) {
+    const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(base + lo_off));
+    const i16x4 up = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(base + hi_off));
+    typedef __attribute__((ext_vector_type(8))) short i16x8;
+    i16x8 v = {lo[0], lo[1], lo[2], lo[3], up[0], up[1], up[2], up[3]};
+    return __builtin_bit_cast(bf16x8, v);
+  };
+
   // dP's accumulator starts at -delta of its rows (the tile's LSE/delta piece), so the chain yields
   // dP - delta directly
   auto sdp = [&](int si, f32x16& s, f32x16& dp) __attribute__((always_inline)) {
@@ -373,9 +410,9 @@ __global__ __launch_bounds__(BwdCfg<D>::NTH, bwd_waves_per_eu<D>()) void attn_bw
       bf16x8 qa[KS], kbf[KS], da[KS];
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
-        qa[ks] = lds_read_b128(qs, lds_off<D>(r, 2 * ks + h));
-        kbf[ks] = lds_read_b128(kimg, kimg_off<D>(32 * wave + r, 2 * ks + h));
-        da[ks] = lds_read_b128(dos, lds_off<D>(r, 2 * ks + h));
+        qa[ks] = lds_read_b128(qs, qo[ks]);
+        kbf[ks] = lds_read_b128(kimg, ko[ks]);
+        da[ks] = lds_read_b128(dos, qo[ks]);
       }
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
@@ -428,9 +465,11 @@ __global__ __launch_bounds__(BwdCfg<D>::NTH, bwd_waves_per_eu<D>()) void attn_bw
       sf[st] = pack_frag(sv);
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
-        const bf16x8 dof = lds_read_tr32<D>(dos, 16 * st, 32 * dt, lane);
+        const bf16x8 dof = D == 64 ? tr_pair(dos + 16 * st * C::RB, tro[dt][0], tro[dt][1])
+                                   : lds_read_tr32<D>(dos, 16 * st, 32 * dt, lane);
         dv[dt] = mfma32(pf, dof, dv[dt]);
-        const bf16x8 qf = lds_read_tr32<D>(qs, 16 * st, 32 * dt, lane);
+        const bf16x8 qf = D == 64 ? tr_pair(qs + 16 * st * C::RB, tro[dt][0], tro[dt][1])
+                                  : lds_read_tr32<D>(qs, 16 * st, 32 * dt, lane);
         dk[dt] = mfma32(sf[st], qf, dk[dt]);
       }
     }
@@ -440,13 +479,12 @@ __global__ __launch_bounds__(BwdCfg<D>::NTH, bwd_waves_per_eu<D>()) void attn_bw
   // -> one 8-B store each
   auto ds_write = [&](int par, const bf16x8 (&sf)[2]) __attribute__((always_inline)) {
     char* dsimg = dsimg0 + (unsigned)par * (unsigned)C::DSIMG;
-    const int krow = 32 * wave + r;
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
       const bf16x8 v = sf[g >> 1];
       const bf16x4 w = (g & 1) ? bf16x4{v[4], v[5], v[6], v[7]} : bf16x4{v[0], v[1], v[2], v[3]};
-      *reinterpret_cast<bf16x4*>(dsimg + ds_img_off(krow, 8 * g + 4 * h)) = w;
+      *reinterpret_cast<bf16x4*>(dsimg + dso[g]) = w;
     }
   };
 

@@ -40,7 +40,7 @@ std::atomic<unsigned> g_mask{0};  // bit k set: kernel id k is being timed
 Pool g_pool[PICO_K_COUNT];
 
 void destroy_pool(Pool& p) {
-  for (auto e : p.ev) hipEventDestroy(e);
+  for (auto e : p.ev) (void)hipEventDestroy(e);
   p.ev.clear();
   p.used = p.capacity = 0;
 }
@@ -51,7 +51,7 @@ void pico_prof_pre(int kid, hipStream_t s) {
   std::lock_guard<std::mutex> lk(g_mu);
   Pool& p = g_pool[kid];
   if (p.used >= p.capacity) return;
-  hipEventRecord(p.ev[2 * p.used], s);
+  (void)hipEventRecord(p.ev[2 * p.used], s);
 }
 
 void pico_prof_post(int kid, hipStream_t s) {
@@ -59,7 +59,7 @@ void pico_prof_post(int kid, hipStream_t s) {
   std::lock_guard<std::mutex> lk(g_mu);
   Pool& p = g_pool[kid];
   if (p.used >= p.capacity) return;
-  hipEventRecord(p.ev[2 * p.used + 1], s);
+  (void)hipEventRecord(p.ev[2 * p.used + 1], s);
   p.used++;
 }
 
@@ -106,7 +106,7 @@ int pico_prof_collect(int kernel_id, double* total_ms, int64_t* launches) {
       return (int)r;
     }
     float ms = 0.f;
-    hipEventElapsedTime(&ms, p.ev[2 * i], p.ev[2 * i + 1]);
+    (void)hipEventElapsedTime(&ms, p.ev[2 * i], p.ev[2 * i + 1]);
     tot += ms;
   }
   *total_ms = tot;
