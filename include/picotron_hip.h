@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define PICO_ABI_VERSION 1
+#define PICO_ABI_VERSION 2
 #define PICO_EINVAL 1000
 
 /* kernel ids for the optional event timer (pico_prof_*) */
@@ -143,9 +143,17 @@ typedef struct pico_attn_args {
   float softmax_scale;
   int causal;
   int flags;
+  /* PICO_ATTN_ROPE_BWD: bf16 rotate-half tables [>= S, D/2] (row stride rope_stride elements) */
+  const void* rope_cos;
+  const void* rope_sin;
+  int64_t rope_stride;
 } pico_attn_args;
 
 #define PICO_ATTN_DQ_F32_ACCUM 1 /* dq is fp32 [B,Sq,Hq,D] (dq_strides) and is ADDED into */
+/* bwd: q and k were rotated (RoPE, rotate-half, position = sequence index) before attention; dq and dk
+ * are returned rotated back by -theta (the RoPE backward, ref picotron/model.py:135-136), fused into
+ * the dQ slab sum and the dK epilogue. Not combinable with PICO_ATTN_DQ_F32_ACCUM. */
+#define PICO_ATTN_ROPE_BWD 2
 
 int64_t pico_attn_args_size(void); /* sizeof(pico_attn_args), for FFI layout checks */
 int pico_attn_fwd(const pico_attn_args* args, void* stream);

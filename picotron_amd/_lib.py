@@ -27,6 +27,7 @@ KERNEL_NAMES = {
 }
 
 ATTN_DQ_F32_ACCUM = 1
+ATTN_ROPE_BWD = 2
 
 c_i64 = ctypes.c_int64
 c_vp = ctypes.c_void_p
@@ -42,6 +43,7 @@ class AttnArgs(ctypes.Structure):
         ("q_strides", c_i64 * 3), ("k_strides", c_i64 * 3), ("v_strides", c_i64 * 3), ("o_strides", c_i64 * 3),
         ("do_strides", c_i64 * 3), ("dq_strides", c_i64 * 3), ("dk_strides", c_i64 * 3), ("dv_strides", c_i64 * 3),
         ("softmax_scale", ctypes.c_float), ("causal", ctypes.c_int), ("flags", ctypes.c_int),
+        ("rope_cos", c_vp), ("rope_sin", c_vp), ("rope_stride", c_i64),
     ]
 
 

@@ -605,13 +605,28 @@ __global__ __launch_bounds__(BwdCfg<D>::NTH, bwd_waves_per_eu<D>()) void attn_bw
   if (hsplit == 1) {
     bf16_t* dkg = (bf16_t*)a.dk + b * a.dk_strides[0] + hk * a.dk_strides[2];
     bf16_t* dvg = (bf16_t*)a.dv + b * a.dv_strides[0] + hk * a.dv_strides[2];
+    const bool rope = (a.flags & PICO_ATTN_ROPE_BWD) != 0;  // uniform
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int key = kw + acc_row(i, h);
       if (key < Sk) {
+        float kv[DT];
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) kv[dt] = dk[dt][i] * scale;
+        if (rope) {  // d = 32 dt + r pairs with d + D/2 = 32 (dt + DT/2) + r: both in this lane
+          const bf16_t* cp = (const bf16_t*)a.rope_cos + (int64_t)key * a.rope_stride + r;
+          const bf16_t* sp = (const bf16_t*)a.rope_sin + (int64_t)key * a.rope_stride + r;
+#pragma unroll
+          for (int dt = 0; dt < DT / 2; ++dt) {
+            const float cf = bf2f(cp[32 * dt]), sf = bf2f(sp[32 * dt]);
+            const float u = kv[dt], w = kv[dt + DT / 2];
+            kv[dt] = u * cf + w * sf;
+            kv[dt + DT / 2] = w * cf - u * sf;
+          }
+        }
 #pragma unroll
         for (int dt = 0; dt < DT; ++dt) {
-          dkg[(int64_t)key * a.dk_strides[1] + 32 * dt + r] = f2bf(dk[dt][i] * scale);
+          dkg[(int64_t)key * a.dk_strides[1] + 32 * dt + r] = f2bf(kv[dt]);
           dvg[(int64_t)key * a.dv_strides[1] + 32 * dt + r] = f2bf(dv[dt][i]);
         }
       }
@@ -634,76 +649,110 @@ __global__ __launch_bounds__(BwdCfg<D>::NTH, bwd_waves_per_eu<D>()) void attn_bw
   }
 }
 
+// rotate-half RoPE backward (rotation by -theta) of the pair (x[d], x[d + D/2]), d = i0 + j, j < 8, at
+// sequence position pos: x1' = x1 c + x2 s, x2' = x2 c - x1 s (pico_rope with conjugate = 1)
+PICO_DEV void rope_bwd8(const pico_attn_args& a, int pos, int i0, float* x1, float* x2) {
+  const u16x8 c = *reinterpret_cast<const u16x8*>((const bf16_t*)a.rope_cos + (int64_t)pos * a.rope_stride + i0);
+  const u16x8 sn = *reinterpret_cast<const u16x8*>((const bf16_t*)a.rope_sin + (int64_t)pos * a.rope_stride + i0);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float cf = bf2f(c[j]), sf = bf2f(sn[j]), u = x1[j], w = x2[j];
+    x1[j] = u * cf + w * sf;
+    x2[j] = w * cf - u * sf;
+  }
+}
+
 // dq[b, q, h, :] = sum over key blocks kb (causal: kb * 256 <= q) of the fp32 partial slabs, summed in
-// kb order (deterministic). Writes bf16 (strided), or ADDS into an fp32 accumulator.
+// kb order (deterministic), optionally rotated back (PICO_ATTN_ROPE_BWD). A thread owns the 8-element
+// pair of chunks d0 .. d0+7 and D/2 + d0 .. (so the rotation pairs are local). Writes bf16 (strided), or
+// ADDS into an fp32 accumulator.
 template <int D, bool CAUSAL>
 __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const pico_attn_args a, const float* __restrict__ dq_part,
                                                           int64_t slab, int nkb, int f32acc) {
-  constexpr int LPR = D / 8;
+  constexpr int TPR = D / 16;  // threads per row
   const int64_t rows = a.batch * a.seqlen_q * a.heads_q;
-  const int64_t row = ((int64_t)blockIdx.x * 256 + threadIdx.x) / LPR;
-  const int sub = threadIdx.x % LPR;
+  const int64_t row = ((int64_t)blockIdx.x * 256 + threadIdx.x) / TPR;
+  const int d0 = (threadIdx.x % TPR) * 8;
   if (row >= rows) return;
   const int hq = (int)(row % a.heads_q);
   const int64_t bq = row / a.heads_q;
   const int q = (int)(bq % a.seqlen_q);
   const int b = (int)(bq / a.seqlen_q);
   const int last = CAUSAL ? min(nkb - 1, q / BK) : nkb - 1;
-  f32x4 x0 = (f32x4)0.f, x1 = (f32x4)0.f;
+  float x1[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, x2[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   for (int k = 0; k <= last; ++k) {
-    const f32x4* src = reinterpret_cast<const f32x4*>(dq_part + k * slab + row * D + sub * 8);
-    x0 += src[0];
-    x1 += src[1];
-  }
-  if (f32acc) {
-    float* dst = (float*)a.dq + b * a.dq_strides[0] + q * a.dq_strides[1] + hq * a.dq_strides[2] + sub * 8;
+    const f32x4* lo = reinterpret_cast<const f32x4*>(dq_part + k * slab + row * D + d0);
+    const f32x4* hi = reinterpret_cast<const f32x4*>(dq_part + k * slab + row * D + D / 2 + d0);
+    const f32x4 l0 = lo[0], l1 = lo[1], h0 = hi[0], h1 = hi[1];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      dst[j] += x0[j];
-      dst[4 + j] += x1[j];
+      x1[j] += l0[j];
+      x1[4 + j] += l1[j];
+      x2[j] += h0[j];
+      x2[4 + j] += h1[j];
+    }
+  }
+  if (a.flags & PICO_ATTN_ROPE_BWD) rope_bwd8(a, q, d0, x1, x2);
+  if (f32acc) {
+    float* dst = (float*)a.dq + b * a.dq_strides[0] + q * a.dq_strides[1] + hq * a.dq_strides[2] + d0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      dst[j] += x1[j];
+      dst[D / 2 + j] += x2[j];
     }
     return;
   }
-  u16x8 o;
+  u16x8 o1, o2;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    o[j] = f2bf(x0[j]);
-    o[4 + j] = f2bf(x1[j]);
+  for (int j = 0; j < 8; ++j) {
+    o1[j] = f2bf(x1[j]);
+    o2[j] = f2bf(x2[j]);
   }
-  *reinterpret_cast<u16x8*>((bf16_t*)a.dq + b * a.dq_strides[0] + q * a.dq_strides[1] + hq * a.dq_strides[2] +
-                            sub * 8) = o;
+  bf16_t* dst = (bf16_t*)a.dq + b * a.dq_strides[0] + q * a.dq_strides[1] + hq * a.dq_strides[2] + d0;
+  *reinterpret_cast<u16x8*>(dst) = o1;
+  *reinterpret_cast<u16x8*>(dst + D / 2) = o2;
 }
 
-// dK / dV [b, key, hk, :] = sum over the hsplit workgroups' fp32 partials (fixed order) -> bf16 (strided)
+// dK / dV [b, key, hk, :] = sum over the hsplit workgroups' fp32 partials (fixed order) -> bf16 (strided);
+// dK optionally rotated back (PICO_ATTN_ROPE_BWD). Thread layout as attn_bwd_dq_kernel.
 template <int D>
 __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const pico_attn_args a, const float* __restrict__ dkv_part,
                                                            int hsplit) {
-  constexpr int LPR = D / 8;
+  constexpr int TPR = D / 16;
   const int64_t part = a.batch * a.seqlen_k * a.heads_kv * D;
   const int64_t rows = a.batch * a.seqlen_k * a.heads_kv;
-  const int64_t row = ((int64_t)blockIdx.x * 256 + threadIdx.x) / LPR;
-  const int sub = threadIdx.x % LPR;
+  const int64_t row = ((int64_t)blockIdx.x * 256 + threadIdx.x) / TPR;
+  const int d0 = (threadIdx.x % TPR) * 8;
   if (row >= rows) return;
   const int hk = (int)(row % a.heads_kv);
   const int64_t bk = row / a.heads_kv;
   const int key = (int)(bk % a.seqlen_k);
   const int b = (int)(bk / a.seqlen_k);
   for (int which = 0; which < 2; ++which) {
-    f32x4 x0 = (f32x4)0.f, x1 = (f32x4)0.f;
+    float x1[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, x2[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     for (int hs = 0; hs < hsplit; ++hs) {
-      const f32x4* src = reinterpret_cast<const f32x4*>(dkv_part + (2 * hs + which) * part + row * D + sub * 8);
-      x0 += src[0];
-      x1 += src[1];
-    }
-    u16x8 o;
+      const float* src = dkv_part + (2 * hs + which) * part + row * D + d0;
+      const f32x4 l0 = reinterpret_cast<const f32x4*>(src)[0], l1 = reinterpret_cast<const f32x4*>(src)[1];
+      const f32x4 h0 = reinterpret_cast<const f32x4*>(src + D / 2)[0], h1 = reinterpret_cast<const f32x4*>(src + D / 2)[1];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      o[j] = f2bf(x0[j]);
-      o[4 + j] = f2bf(x1[j]);
+      for (int j = 0; j < 4; ++j) {
+        x1[j] += l0[j];
+        x1[4 + j] += l1[j];
+        x2[j] += h0[j];
+        x2[4 + j] += h1[j];
+      }
+    }
+    if (which == 0 && (a.flags & PICO_ATTN_ROPE_BWD)) rope_bwd8(a, key, d0, x1, x2);
+    u16x8 o1, o2;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      o1[j] = f2bf(x1[j]);
+      o2[j] = f2bf(x2[j]);
     }
     bf16_t* dst = which ? (bf16_t*)a.dv + b * a.dv_strides[0] + key * a.dv_strides[1] + hk * a.dv_strides[2]
                         : (bf16_t*)a.dk + b * a.dk_strides[0] + key * a.dk_strides[1] + hk * a.dk_strides[2];
-    *reinterpret_cast<u16x8*>(dst + sub * 8) = o;
+    *reinterpret_cast<u16x8*>(dst + d0) = o1;
+    *reinterpret_cast<u16x8*>(dst + d0 + D / 2) = o2;
   }
 }
 
@@ -737,7 +786,7 @@ int launch_bwd(const pico_attn_args* a, hipStream_t s) {
   float* trash = dq_part + (int64_t)((a->seqlen_k + BK - 1) / BK) * a->batch * a->seqlen_q * a->heads_q * D;
   const int64_t slab = a->batch * a->seqlen_q * a->heads_q * D;
   const int64_t rows = a->batch * a->seqlen_q * a->heads_q;
-  const int row_blocks = pico_cdiv(rows * (D / 8), 256);
+  const int row_blocks = pico_cdiv(rows * (D / 16), 256);  // attn_bwd_dq_kernel: D/16 threads per row
   const int pre_blocks = pico_cdiv(a->batch * a->heads_q * (int64_t)sq_pad * (D / 8), 256);
   PICO_LAUNCH(PICO_K_ATTN_BWD_PRE, "attn_bwd_pre", s,
               attn_bwd_pre_kernel<D><<<pre_blocks, 256, 0, s>>>(*a, delta, lse2, sq_pad));
@@ -758,7 +807,7 @@ int launch_bwd(const pico_attn_args* a, hipStream_t s) {
                       *a, a->softmax_scale, sl2, delta, lse2, sq_pad, dq_part, slab, trash, hsplit, dkv_part));
     }
     if (hsplit > 1) {
-      const int kv_blocks = pico_cdiv(a->batch * a->seqlen_k * a->heads_kv * (D / 8), 256);
+      const int kv_blocks = pico_cdiv(a->batch * a->seqlen_k * a->heads_kv * (D / 16), 256);
       PICO_LAUNCH(PICO_K_ATTN_BWD_DKV, "attn_bwd_dkv", s,
                   attn_bwd_dkv_kernel<D><<<kv_blocks, 256, 0, s>>>(*a, dkv_part, hsplit));
     }
@@ -817,6 +866,13 @@ int pico_attn_bwd(const pico_attn_args* a, void* stream) {
     for (int d = 0; d < 3; ++d)
       PICO_REQUIRE(st[i][d] % 8 == 0 || (i == 2 && (a->flags & PICO_ATTN_DQ_F32_ACCUM)),
                    "pico_attn_bwd: strides must be multiples of 8 elements");
+  if (a->flags & PICO_ATTN_ROPE_BWD) {
+    PICO_REQUIRE(!(a->flags & PICO_ATTN_DQ_F32_ACCUM), "pico_attn_bwd: ROPE_BWD cannot be combined with DQ_F32_ACCUM");
+    PICO_REQUIRE(a->rope_cos && a->rope_sin && ((uintptr_t)a->rope_cos | (uintptr_t)a->rope_sin) % 16 == 0,
+                 "pico_attn_bwd: ROPE_BWD needs 16-byte aligned cos/sin tables");
+    PICO_REQUIRE(a->rope_stride % 8 == 0 && a->rope_stride >= a->head_dim / 2,
+                 "pico_attn_bwd: bad rope table row stride %lld", (long long)a->rope_stride);
+  }
   if (a->batch == 0 || a->seqlen_q == 0 || a->heads_q == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   if (a->head_dim == 64) return launch_bwd<64>(a, s);

@@ -692,8 +692,8 @@ class _QKVRopeAttentionFn(torch.autograd.Function):
     """The attention block's hot path in one autograd node:
       qkv = x [Wq; Wk; Wv]^T (ONE GEMM) -> RoPE in place on the q|k columns (ONE launch, q and k heads
       are adjacent in qkv) -> flash attention reading q/k/v as strided views of qkv.
-    Backward: attention writes dq/dk/dv straight into the column blocks of one dqkv buffer, RoPE^-1
-    runs in place on dq|dk, then dx = dqkv W (one GEMM, no sum of three dgrads) and
+    Backward: attention writes dq/dk/dv straight into the column blocks of one dqkv buffer with RoPE^-1
+    applied inside it (dQ slab sum, dK epilogue), then dx = dqkv W (one GEMM, no sum of three dgrads) and
     dW = dqkv^T x (one GEMM, rows = dWq | dWk | dWv)."""
 
     @staticmethod
@@ -725,10 +725,15 @@ class _QKVRopeAttentionFn(torch.autograd.Function):
         q, k, v = heads[:, :, :nh], heads[:, :, nh:nh + nkv], heads[:, :, nh + nkv:]
         dqkv = torch.empty_like(qkv)
         dheads = dqkv.view(B, S, N // D, D)
+        # RoPE^-1 on dq | dk fused into the attention backward's dQ sum and dK epilogue
+        # (PICO_FUSE_ROPE_BWD=0: separate in-place rope launch, for A/B)
+        fused = os.getenv("PICO_FUSE_ROPE_BWD", "1") != "0"
         _attention_bwd_into(do.reshape(B, S, nh, D), q, k, v, o, lse, scale, causal,
-                            dheads[:, :, :nh], dheads[:, :, nh:nh + nkv], dheads[:, :, nh + nkv:])
-        dqk = dheads[:, :, : nh + nkv]
-        _rope_launch(dqk, dqk, cos, sin, True)
+                            dheads[:, :, :nh], dheads[:, :, nh:nh + nkv], dheads[:, :, nh + nkv:],
+                            rope=(cos, sin) if fused else None)
+        if not fused:
+            dqk = dheads[:, :, : nh + nkv]
+            _rope_launch(dqk, dqk, cos, sin, True)
         dx = dgrad(dqkv, W, ctx.params).view(B, S, Hd)
         dwq, dwk, dwv = wgrad_accumulate(ctx.params, dqkv, x2)
         return dx, dwq, dwk, dwv, None, None, None, None, None
@@ -741,8 +746,10 @@ def qkv_rope_attention(x, wq, wk, wv, cos, sin, num_heads, num_kv_heads, causal)
                                      causal)
 
 
-def _attention_bwd_into(dout, q, k, v, o, lse, softmax_scale, causal, dq, dk, dv):
-    """attention backward writing into caller-provided (possibly strided) dq/dk/dv."""
+def _attention_bwd_into(dout, q, k, v, o, lse, softmax_scale, causal, dq, dk, dv, rope=None):
+    """attention backward writing into caller-provided (possibly strided) dq/dk/dv. rope = (cos, sin)
+    ([>= S, D/2] bf16 tables): q and k were rotated before the forward; dq and dk come back rotated by
+    -theta (the RoPE backward fused into the dQ sum and the dK epilogue, PICO_ATTN_ROPE_BWD)."""
     if dout.stride(-1) != 1 or any(s_ % 8 for s_ in dout.stride()[:3]):
         dout = dout.contiguous()
     a = _attn_args(q, k, v, o, lse, softmax_scale, causal)
@@ -752,6 +759,14 @@ def _attention_bwd_into(dout, q, k, v, o, lse, softmax_scale, causal, dq, dk, dv
     a.dq_strides = _lib.i64x3(dq.stride()[:3])
     a.dk_strides = _lib.i64x3(dk.stride()[:3])
     a.dv_strides = _lib.i64x3(dv.stride()[:3])
+    if rope is not None:
+        cos, sin = rope
+        _need(cos, "cos")
+        _need(sin, "sin")
+        if cos.stride(1) != 1 or sin.stride(0) != cos.stride(0) or cos.shape[1] * 2 != q.shape[3]:
+            raise ValueError("attention rope backward: cos/sin must be [>= S, D/2] with unit column stride")
+        a.flags |= _lib.ATTN_ROPE_BWD
+        a.rope_cos, a.rope_sin, a.rope_stride = _lib.ptr(cos), _lib.ptr(sin), cos.stride(0)
     lib = _lib.load()
     ws = torch.empty(lib.pico_attn_bwd_workspace_bytes(ctypes.byref(a)), dtype=torch.uint8, device=q.device)
     a.workspace = _lib.ptr(ws)

@@ -32,7 +32,7 @@ def test_exports_every_declared_symbol(lib):
     for n in names:
         assert hasattr(lib, n), n
         assert n in _lib.EXPORTED_SYMBOLS, f"{n} has no ctypes signature"
-    assert lib.pico_abi_version() == 1
+    assert lib.pico_abi_version() == 2  # 2: pico_attn_args gained the RoPE-backward table fields
 
 
 def test_struct_layout_matches(lib):

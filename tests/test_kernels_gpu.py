@@ -460,3 +460,30 @@ def test_transpose_bit_exact(R, C, ld_pad):
     if ld_pad:
         assert bool((out_base[:, R:] == 7.0).all())
     assert torch.equal(ops.transpose_2d(x), x.t().contiguous())
+
+
+# ------------------------------------------------------------------------------------------ fused RoPE backward
+@pytest.mark.parametrize("B,S,Hq,Hkv,D", [(4, 1024, 32, 32, 64), (2, 256, 4, 2, 64), (1, 384, 4, 4, 128)])
+def test_attention_rope_bwd_fused(B, S, Hq, Hkv, D):
+    """PICO_ATTN_ROPE_BWD (RoPE^-1 fused into the dQ slab sum and the dK epilogue / dK-dV reduce, both
+    the one-workgroup-per-key-block grid and the split small grid) == attention backward followed by the
+    separate pico_rope(conjugate=1) on dq and dk, within one bf16 rounding; dv untouched."""
+    from picotron_amd import ops
+    from picotron_amd.model import get_cos_sin
+    torch.manual_seed(S + D)
+    q, do = [torch.randn(B, S, Hq, D, dtype=BF, device=DEV) for _ in range(2)]
+    k, v = [torch.randn(B, S, Hkv, D, dtype=BF, device=DEV) for _ in range(2)]
+    cos, sin = get_cos_sin(S, D, base=10000.0)
+    cos, sin = cos.to(DEV, BF)[:, : D // 2], sin.to(DEV, BF)[:, : D // 2]
+    sc = 1.0 / math.sqrt(D)
+    o, lse = ops.attention_block_fwd(q, k, v, sc, True)
+    dq0, dk0, dv0 = ops.attention_block_bwd(do, q, k, v, o, lse, sc, True)
+    ref_dq, ref_dk = torch.empty_like(dq0), torch.empty_like(dk0)
+    ops._rope_launch(dq0, ref_dq, cos, sin, True)
+    ops._rope_launch(dk0, ref_dk, cos, sin, True)
+    dq, dk, dv = [torch.empty_like(t) for t in (q, k, v)]
+    ops._attention_bwd_into(do, q, k, v, o, lse, sc, True, dq, dk, dv, rope=(cos, sin))
+    torch.cuda.synchronize()
+    assert torch.equal(dv, dv0)
+    assert rel_l2(dq.float().cpu(), ref_dq.float().cpu()) < 4e-3
+    assert rel_l2(dk.float().cpu(), ref_dk.float().cpu()) < 4e-3
