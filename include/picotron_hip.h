@@ -147,6 +147,11 @@ typedef struct pico_attn_args {
   const void* rope_cos;
   const void* rope_sin;
   int64_t rope_stride;
+  /* fwd, optional (NULL: off): O also written transposed, o_t[hq * D + d][b * Sq + q] with row stride
+   * o_t_ld elements — the [Hq*D, tokens] layout of the out-projection input that its weight-gradient
+   * GEMM reads fastest (x^T), written from the accumulator layout at no extra pass */
+  void* o_t;
+  int64_t o_t_ld;
 } pico_attn_args;
 
 #define PICO_ATTN_DQ_F32_ACCUM 1 /* dq is fp32 [B,Sq,Hq,D] (dq_strides) and is ADDED into */

@@ -43,7 +43,7 @@ class AttnArgs(ctypes.Structure):
         ("q_strides", c_i64 * 3), ("k_strides", c_i64 * 3), ("v_strides", c_i64 * 3), ("o_strides", c_i64 * 3),
         ("do_strides", c_i64 * 3), ("dq_strides", c_i64 * 3), ("dk_strides", c_i64 * 3), ("dv_strides", c_i64 * 3),
         ("softmax_scale", ctypes.c_float), ("causal", ctypes.c_int), ("flags", ctypes.c_int),
-        ("rope_cos", c_vp), ("rope_sin", c_vp), ("rope_stride", c_i64),
+        ("rope_cos", c_vp), ("rope_sin", c_vp), ("rope_stride", c_i64), ("o_t", c_vp), ("o_t_ld", c_i64),
     ]
 
 

@@ -332,6 +332,16 @@ __attribute__((amdgpu_waves_per_eu(FwdCfg<D>::WAVES_PER_EU, FwdCfg<D>::WAVES_PER
         *reinterpret_cast<u16x4*>(op + 32 * dt + 8 * g + 4 * h) = w;
       }
     }
+    if (a.o_t) {  // uniform: O^T [Hq*D][tokens]; lanes r = 0..31 are consecutive tokens (64-B segments)
+      bf16_t* ot = (bf16_t*)a.o_t + (int64_t)hq * D * a.o_t_ld + (int64_t)b * Sq + my_q;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int d = 32 * dt + 8 * (i >> 2) + 4 * h + (i & 3);
+          ot[(int64_t)d * a.o_t_ld] = f2bf(o[dt][i] * inv);
+        }
+    }
     if (h == 0) {
       const float lse = l_tot > 0.f ? (m_i + __log2f(l_tot)) * LN2 : -INFINITY;
       a.lse[((int64_t)b * a.heads_q + hq) * Sq + my_q] = lse;
@@ -362,6 +372,7 @@ extern "C" int pico_attn_fwd(const pico_attn_args* a, void* stream) {
   int rc = pico_attn_check_common(a, "pico_attn_fwd");
   if (rc) return rc;
   PICO_REQUIRE(a->o && a->lse, "pico_attn_fwd: null output");
+  PICO_REQUIRE(!a->o_t || a->o_t_ld >= a->batch * a->seqlen_q, "pico_attn_fwd: o_t_ld must cover the tokens");
   if (a->batch == 0 || a->seqlen_q == 0 || a->heads_q == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   if (a->head_dim == 64) return launch_fwd<64>(a, s);

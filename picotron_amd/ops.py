@@ -371,11 +371,16 @@ def transpose_2d(x, out=None):
     return out
 
 
-def _wgrad_input(x2, n_out):
+def _wgrad_input(x2, n_out, x=None):
     """What the backward keeps of a projection's input x2 [T, K] for its wgrad: x2 itself, or x2^T as a
     transposed view of a contiguous [K, T] copy where hipBLASLt's "TT" wgrad form saves more than the
     transpose costs (output width >= 3 K: qkv, gate|up, LM head; gemm_layout_probe.py --wgrad)."""
-    if os.getenv("PICO_XT_WGRAD", "1") != "0" and n_out >= 3 * x2.shape[1] and x2.is_cuda:
+    if os.getenv("PICO_XT_WGRAD", "1") == "0" or not x2.is_cuda:
+        return x2
+    xt = getattr(x, "_pico_t", None)  # a producer wrote x^T as a by-product (attention output)
+    if xt is not None and tuple(xt.shape) == (x2.shape[1], x2.shape[0]):
+        return xt.t()
+    if n_out >= 3 * x2.shape[1]:
         return transpose_2d(x2).t()
     return x2
 
@@ -497,7 +502,7 @@ class _LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w):
         x2 = x.reshape(-1, x.shape[-1])
-        ctx.save_for_backward(_wgrad_input(x2, w.shape[0]) if ctx.needs_input_grad[1] else x2, w)
+        ctx.save_for_backward(_wgrad_input(x2, w.shape[0], x) if ctx.needs_input_grad[1] else x2, w)
         ctx.xshape = x.shape
         return torch.nn.functional.linear(x, w)
 
@@ -616,8 +621,9 @@ def _check_qkv(q, k, v):
         raise ValueError("flash attention: heads_q must be a multiple of heads_kv")
 
 
-def attention_block_fwd(q, k, v, softmax_scale, causal):
-    """O [B,Sq,Hq,D] bf16 and LSE [B,Hq,Sq] fp32 (natural log) of softmax(scale*QK^T [+causal]) V."""
+def attention_block_fwd(q, k, v, softmax_scale, causal, o_t=None):
+    """O [B,Sq,Hq,D] bf16 and LSE [B,Hq,Sq] fp32 (natural log) of softmax(scale*QK^T [+causal]) V.
+    o_t (optional, bf16 [Hq*D, >= B*Sq] with unit column stride) also receives O transposed."""
     _check_qkv(q, k, v)
     q, k, v = [t if t.stride(-1) == 1 and all(s % 8 == 0 for s in t.stride()[:3]) else t.contiguous()
                for t in (q, k, v)]
@@ -625,6 +631,11 @@ def attention_block_fwd(q, k, v, softmax_scale, causal):
     o = torch.empty((B, Sq, Hq, D), dtype=q.dtype, device=q.device)
     lse = torch.empty((B, Hq, Sq), dtype=torch.float32, device=q.device)
     a = _attn_args(q, k, v, o, lse, softmax_scale, causal)
+    if o_t is not None:
+        _need(o_t, "o_t")
+        if o_t.shape[0] != Hq * D or o_t.stride(1) != 1 or o_t.shape[1] < B * Sq:
+            raise ValueError("attention_block_fwd: o_t must be [Hq*D, >= B*Sq] with unit column stride")
+        a.o_t, a.o_t_ld = _lib.ptr(o_t), o_t.stride(0)
     _lib.check(_lib.load().pico_attn_fwd(ctypes.byref(a), _lib.stream_of(q)), "pico_attn_fwd")
     return o, lse
 
@@ -710,11 +721,17 @@ class _QKVRopeAttentionFn(torch.autograd.Function):
         heads = qkv.view(B, S, N // D, D)
         q, k, v = heads[:, :, :nh], heads[:, :, nh:nh + nkv], heads[:, :, nh + nkv:]
         scale = 1.0 / math.sqrt(D)
-        o, lse = attention_block_fwd(q, k, v, scale, causal)
+        # O^T for the out-projection's wgrad (TT form), written by the attention epilogue for free
+        o_t = torch.empty((nh * D, B * S), dtype=x.dtype, device=x.device) \
+            if os.getenv("PICO_XT_WGRAD", "1") != "0" else None
+        o, lse = attention_block_fwd(q, k, v, scale, causal, o_t=o_t)
         ctx.save_for_backward(_wgrad_input(x2, N), W, qkv, o, lse, cos, sin)
         ctx.params = (wq, wk, wv)
         ctx.meta = (B, S, Hd, nh, nkv, D, causal, scale)
-        return o.view(B, S, nh * D)
+        out = o.view(B, S, nh * D)
+        if o_t is not None:
+            out._pico_t = o_t
+        return out
 
     @staticmethod
     def backward(ctx, do):

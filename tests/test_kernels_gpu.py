@@ -487,3 +487,18 @@ def test_attention_rope_bwd_fused(B, S, Hq, Hkv, D):
     assert torch.equal(dv, dv0)
     assert rel_l2(dq.float().cpu(), ref_dq.float().cpu()) < 4e-3
     assert rel_l2(dk.float().cpu(), ref_dk.float().cpu()) < 4e-3
+
+
+@pytest.mark.parametrize("B,S,H,D,causal", [(2, 256, 4, 64, True), (1, 200, 2, 128, False)])
+def test_attention_fwd_transposed_output(B, S, H, D, causal):
+    """pico_attn_fwd's optional o_t output == O transposed to [H*D, tokens], bit for bit (same rounding),
+    and O itself unchanged by requesting it."""
+    from picotron_amd import ops
+    torch.manual_seed(S)
+    q, k, v = [torch.randn(B, S, H, D, dtype=BF, device=DEV) for _ in range(3)]
+    o_ref, lse_ref = ops.attention_block_fwd(q, k, v, 0.1, causal)
+    o_t = torch.full((H * D, B * S + 8), 3.0, dtype=BF, device=DEV)[:, : B * S]
+    o, lse = ops.attention_block_fwd(q, k, v, 0.1, causal, o_t=o_t)
+    torch.cuda.synchronize()
+    assert torch.equal(o, o_ref) and torch.equal(lse, lse_ref)
+    assert torch.equal(o_t, o.reshape(B * S, H * D).t())
