@@ -116,6 +116,10 @@ int pico_rope(const void* x, void* out, const void* cos, const void* sin, int64_
 /* ---- SwiGLU epilogue: h = silu(g) * u on [rows, cols] bf16 ----
  * gate/up (and dgate/dup) rows at element stride in_stride (they may be the two column halves of one
  * fused gate|up GEMM output, in_stride = 2*cols); out/dout rows at out_stride. */
+/* pico_swiglu_fwd that also writes out^T ([cols, rows], row stride t_stride): the down projection's
+ * x^T for its weight-gradient GEMM. rows, cols multiples of 64; strides multiples of 8. */
+int pico_swiglu_fwd_t(const void* gate, const void* up, void* out, void* out_t, int64_t rows, int64_t cols,
+                      int64_t in_stride, int64_t out_stride, int64_t t_stride, void* stream);
 int pico_swiglu_fwd(const void* gate, const void* up, void* out, int64_t rows, int64_t cols,
                     int64_t in_stride, int64_t out_stride, void* stream);
 int pico_swiglu_bwd(const void* dout, const void* gate, const void* up, void* dgate, void* dup,

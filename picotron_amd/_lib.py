@@ -61,6 +61,7 @@ _SIGNATURES = {
     "pico_rope": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64,
                                  ctypes.POINTER(c_i64), ctypes.POINTER(c_i64), c_i64, ctypes.c_int, c_vp]),
     "pico_swiglu_fwd": (ctypes.c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp]),
+    "pico_swiglu_fwd_t": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp]),
     "pico_swiglu_bwd": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp]),
     "pico_attn_args_size": (c_i64, []),
     "pico_attn_fwd": (ctypes.c_int, [ctypes.POINTER(AttnArgs), c_vp]),

@@ -69,6 +69,46 @@ __global__ __launch_bounds__(256) void swiglu_bwd_kernel(const bf16_t* __restric
   }
 }
 
+// Forward that also writes h^T ([cols, rows], row stride ts) for the down projection's weight-gradient
+// GEMM (its fast TT form reads x^T). One 256-thread workgroup per 64 x 64 tile: 16-byte loads of the
+// gate/up tile rows, h stored row-major, then the bf16 tile goes through LDS (66-element pitch, the
+// transpose kernel's conflict-free layout) and is stored as 64 rows of h^T (128-B segments).
+// Requires rows, cols multiple of 64 (host checks). Bytes: 3 * 2 B + 2 B (h^T) per element.
+__global__ __launch_bounds__(256) void swiglu_fwd_t_kernel(const bf16_t* __restrict__ g, const bf16_t* __restrict__ u,
+                                                           bf16_t* __restrict__ h, bf16_t* __restrict__ ht, int64_t is,
+                                                           int64_t os, int64_t ts) {
+  __shared__ unsigned short tile[64 * 66];
+  const int64_t r0 = (int64_t)blockIdx.y * 64, c0 = (int64_t)blockIdx.x * 64;
+  const int t = threadIdx.x;
+  const int lr = t >> 3, lc = (t & 7) * 8;
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int64_t row = r0 + lr + 32 * p;
+    const u16x8 gv = *reinterpret_cast<const u16x8*>(g + row * is + c0 + lc);
+    const u16x8 uv = *reinterpret_cast<const u16x8*>(u + row * is + c0 + lc);
+    u16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float gf = bf2f(gv[j]);
+      o[j] = f2bf(gf * sigmoidf_(gf) * bf2f(uv[j]));
+    }
+    *reinterpret_cast<u16x8*>(h + row * os + c0 + lc) = o;
+    unsigned* d = reinterpret_cast<unsigned*>(tile + (lr + 32 * p) * 66 + lc);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) d[k] = (unsigned)o[2 * k] | ((unsigned)o[2 * k + 1] << 16);
+  }
+  __syncthreads();
+  const int oc = t >> 3, ch = (t & 7) * 8;
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int c = oc + 32 * p;
+    u16x8 w;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = tile[(ch + i) * 66 + c];
+    *reinterpret_cast<u16x8*>(ht + (c0 + c) * ts + r0 + ch) = w;
+  }
+}
+
 // scalar fallback (unaligned / ragged shapes)
 __global__ __launch_bounds__(256) void swiglu_fwd_scalar(const bf16_t* __restrict__ g, const bf16_t* __restrict__ u,
                                                          bf16_t* __restrict__ h, int64_t rows, int cols, int64_t is,
@@ -111,6 +151,26 @@ bool vec_ok(int64_t cols, int64_t is, int64_t os, const void* a, const void* b, 
 }  // namespace
 
 extern "C" {
+
+int pico_swiglu_fwd_t(const void* gate, const void* up, void* out, void* out_t, int64_t rows, int64_t cols,
+                      int64_t in_stride, int64_t out_stride, int64_t t_stride, void* stream) {
+  PICO_REQUIRE(gate && up && out && out_t, "pico_swiglu_fwd_t: null pointer");
+  PICO_REQUIRE(rows >= 0 && cols >= 0 && rows % 64 == 0 && cols % 64 == 0,
+               "pico_swiglu_fwd_t: rows and cols must be multiples of 64");
+  PICO_REQUIRE(in_stride >= cols && out_stride >= cols && t_stride >= rows && in_stride % 8 == 0 &&
+                   out_stride % 8 == 0 && t_stride % 8 == 0,
+               "pico_swiglu_fwd_t: strides must cover the matrix and be multiples of 8");
+  PICO_REQUIRE((((uintptr_t)gate | (uintptr_t)up | (uintptr_t)out | (uintptr_t)out_t) & 15) == 0,
+               "pico_swiglu_fwd_t: pointers must be 16-byte aligned");
+  PICO_REQUIRE(rows / 64 <= 65535, "pico_swiglu_fwd_t: too many rows");
+  if (rows == 0 || cols == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  dim3 grid((unsigned)(cols / 64), (unsigned)(rows / 64));
+  PICO_LAUNCH(PICO_K_SWIGLU_FWD, "swiglu_fwd_t", s,
+              swiglu_fwd_t_kernel<<<grid, 256, 0, s>>>((const bf16_t*)gate, (const bf16_t*)up, (bf16_t*)out,
+                                                       (bf16_t*)out_t, in_stride, out_stride, t_stride));
+  return 0;
+}
 
 int pico_swiglu_fwd(const void* gate, const void* up, void* out, int64_t rows, int64_t cols, int64_t in_stride,
                     int64_t out_stride, void* stream) {

@@ -561,12 +561,24 @@ class _GateUpSwiGLUFn(torch.autograd.Function):
         W = stacked_weight((w_gate, w_up))
         x2 = x.reshape(-1, x.shape[-1])
         gu = torch.matmul(x2, W.t())  # [T, 2I]
-        h = torch.empty((x2.shape[0], I), dtype=x.dtype, device=x.device)
-        _swiglu_fwd(gu, gu[:, I:], h, gu.shape[0], I, 2 * I, I)
+        T = gu.shape[0]
+        h = torch.empty((T, I), dtype=x.dtype, device=x.device)
+        ht = None
+        if os.getenv("PICO_XT_WGRAD", "1") != "0" and os.getenv("PICO_SWIGLU_T", "1") != "0" and T % 64 == 0 \
+                and I % 64 == 0 and gu.data_ptr() % 16 == 0:
+            # h^T as a by-product (the down projection's wgrad reads it in the TT GEMM form)
+            ht = torch.empty((I, T), dtype=x.dtype, device=x.device)
+            _lib.check(_lib.load().pico_swiglu_fwd_t(_lib.ptr(gu), _lib.ptr(gu[:, I:]), _lib.ptr(h), _lib.ptr(ht), T, I,
+                                                     2 * I, I, T, _lib.stream_of(gu)), "pico_swiglu_fwd_t")
+        else:
+            _swiglu_fwd(gu, gu[:, I:], h, T, I, 2 * I, I)
         ctx.save_for_backward(_wgrad_input(x2, 2 * I), gu, W)
         ctx.params = (w_gate, w_up)
         ctx.xshape = x.shape
-        return h.view(*x.shape[:-1], I)
+        out = h.view(*x.shape[:-1], I)
+        if ht is not None:
+            out._pico_t = ht
+        return out
 
     @staticmethod
     def backward(ctx, dh):

@@ -502,3 +502,22 @@ def test_attention_fwd_transposed_output(B, S, H, D, causal):
     torch.cuda.synchronize()
     assert torch.equal(o, o_ref) and torch.equal(lse, lse_ref)
     assert torch.equal(o_t, o.reshape(B * S, H * D).t())
+
+
+def test_swiglu_fwd_transposed_output():
+    """pico_swiglu_fwd_t == pico_swiglu_fwd bit for bit on h, and writes h^T exactly (fused gate|up layout)."""
+    from picotron_amd import _lib as L
+    from picotron_amd import ops
+    torch.manual_seed(5)
+    T, I = 256, 512
+    gu = torch.randn(T, 2 * I, dtype=BF, device=DEV)
+    h_ref = torch.empty(T, I, dtype=BF, device=DEV)
+    ops._swiglu_fwd(gu, gu[:, I:], h_ref, T, I, 2 * I, I)
+    h = torch.empty(T, I, dtype=BF, device=DEV)
+    ht = torch.full((I, T + 16), 2.0, dtype=BF, device=DEV)
+    L.check(L.load().pico_swiglu_fwd_t(L.ptr(gu), L.ptr(gu[:, I:]), L.ptr(h), L.ptr(ht), T, I, 2 * I, I, T + 16,
+                                       L.stream_of(gu)), "swiglu_fwd_t")
+    torch.cuda.synchronize()
+    assert torch.equal(h, h_ref)
+    assert torch.equal(ht[:, :T], h.t())
+    assert bool((ht[:, T:] == 2.0).all())
