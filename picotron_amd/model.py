@@ -221,8 +221,9 @@ class DecoderLayer(nn.Module):
         the layer input is residual + delta (residual None for the first layer). Returns the
         (delta, residual) pair whose sum is this layer's output; every sum is rounded to bf16 exactly
         like the reference's `x + f(x)`."""
-        if residual is None:
-            h_in, x = self.input_layernorm(delta), delta
+        if residual is None:  # prenorm form without a residual: x is the norm's second output, so the
+            # embedding output has one consumer and its gradient needs no separate add
+            h_in, x = self.input_layernorm(delta, residual=None, prenorm=True)
         else:
             h_in, x = self.input_layernorm(delta, residual=residual, prenorm=True)
         attn = self.attention(h_in, self.cos, self.sin)
