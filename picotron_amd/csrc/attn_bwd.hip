@@ -605,28 +605,15 @@ __global__ __launch_bounds__(BwdCfg<D>::NTH, bwd_waves_per_eu<D>()) void attn_bw
   if (hsplit == 1) {
     bf16_t* dkg = (bf16_t*)a.dk + b * a.dk_strides[0] + hk * a.dk_strides[2];
     bf16_t* dvg = (bf16_t*)a.dv + b * a.dv_strides[0] + hk * a.dv_strides[2];
-    const bool rope = (a.flags & PICO_ATTN_ROPE_BWD) != 0;  // uniform
+    // (PICO_ATTN_ROPE_BWD: dK is rotated back afterwards by the dQ-sum launch, which also covers
+    // the dK rows — table gathers in this epilogue cost more than that pass)
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int key = kw + acc_row(i, h);
       if (key < Sk) {
-        float kv[DT];
-#pragma unroll
-        for (int dt = 0; dt < DT; ++dt) kv[dt] = dk[dt][i] * scale;
-        if (rope) {  // d = 32 dt + r pairs with d + D/2 = 32 (dt + DT/2) + r: both in this lane
-          const bf16_t* cp = (const bf16_t*)a.rope_cos + (int64_t)key * a.rope_stride + r;
-          const bf16_t* sp = (const bf16_t*)a.rope_sin + (int64_t)key * a.rope_stride + r;
-#pragma unroll
-          for (int dt = 0; dt < DT / 2; ++dt) {
-            const float cf = bf2f(cp[32 * dt]), sf = bf2f(sp[32 * dt]);
-            const float u = kv[dt], w = kv[dt + DT / 2];
-            kv[dt] = u * cf + w * sf;
-            kv[dt + DT / 2] = w * cf - u * sf;
-          }
-        }
 #pragma unroll
         for (int dt = 0; dt < DT; ++dt) {
-          dkg[(int64_t)key * a.dk_strides[1] + 32 * dt + r] = f2bf(kv[dt]);
+          dkg[(int64_t)key * a.dk_strides[1] + 32 * dt + r] = f2bf(dk[dt][i] * scale);
           dvg[(int64_t)key * a.dv_strides[1] + 32 * dt + r] = f2bf(dv[dt][i]);
         }
       }
@@ -666,14 +653,41 @@ PICO_DEV void rope_bwd8(const pico_attn_args& a, int pos, int i0, float* x1, flo
 // kb order (deterministic), optionally rotated back (PICO_ATTN_ROPE_BWD). A thread owns the 8-element
 // pair of chunks d0 .. d0+7 and D/2 + d0 .. (so the rotation pairs are local). Writes bf16 (strided), or
 // ADDS into an fp32 accumulator.
+// rope_dk: the grid also covers the B * Sk * Hkv rows of dK (written un-rotated by attn_bwd_kernel's
+// epilogue), rotated back in place.
 template <int D, bool CAUSAL>
 __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const pico_attn_args a, const float* __restrict__ dq_part,
-                                                          int64_t slab, int nkb, int f32acc) {
+                                                          int64_t slab, int nkb, int f32acc, int rope_dk) {
   constexpr int TPR = D / 16;  // threads per row
   const int64_t rows = a.batch * a.seqlen_q * a.heads_q;
   const int64_t row = ((int64_t)blockIdx.x * 256 + threadIdx.x) / TPR;
   const int d0 = (threadIdx.x % TPR) * 8;
-  if (row >= rows) return;
+  if (row >= rows) {
+    const int64_t kr = row - rows;
+    if (!rope_dk || kr >= a.batch * a.seqlen_k * a.heads_kv) return;
+    const int hk = (int)(kr % a.heads_kv);
+    const int64_t bk = kr / a.heads_kv;
+    const int key = (int)(bk % a.seqlen_k);
+    const int b = (int)(bk / a.seqlen_k);
+    bf16_t* p = (bf16_t*)a.dk + b * a.dk_strides[0] + key * a.dk_strides[1] + hk * a.dk_strides[2] + d0;
+    const u16x8 v1 = *reinterpret_cast<const u16x8*>(p), v2 = *reinterpret_cast<const u16x8*>(p + D / 2);
+    float x1[8], x2[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      x1[j] = bf2f(v1[j]);
+      x2[j] = bf2f(v2[j]);
+    }
+    rope_bwd8(a, key, d0, x1, x2);
+    u16x8 o1, o2;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      o1[j] = f2bf(x1[j]);
+      o2[j] = f2bf(x2[j]);
+    }
+    *reinterpret_cast<u16x8*>(p) = o1;
+    *reinterpret_cast<u16x8*>(p + D / 2) = o2;
+    return;
+  }
   const int hq = (int)(row % a.heads_q);
   const int64_t bq = row / a.heads_q;
   const int q = (int)(bq % a.seqlen_q);
@@ -786,7 +800,11 @@ int launch_bwd(const pico_attn_args* a, hipStream_t s) {
   float* trash = dq_part + (int64_t)((a->seqlen_k + BK - 1) / BK) * a->batch * a->seqlen_q * a->heads_q * D;
   const int64_t slab = a->batch * a->seqlen_q * a->heads_q * D;
   const int64_t rows = a->batch * a->seqlen_q * a->heads_q;
-  const int row_blocks = pico_cdiv(rows * (D / 16), 256);  // attn_bwd_dq_kernel: D/16 threads per row
+  // attn_bwd_dq_kernel: D/16 threads per row; with ROPE_BWD on the one-workgroup-per-key-block grid it
+  // also rotates the dK rows (the split grid's attn_bwd_dkv_kernel already did)
+  const int rope_dk = (a->flags & PICO_ATTN_ROPE_BWD) && hsplit_for(a) == 1;
+  const int64_t kv_rows = rope_dk ? a->batch * a->seqlen_k * a->heads_kv : 0;
+  const int row_blocks = pico_cdiv((rows + kv_rows) * (D / 16), 256);
   const int pre_blocks = pico_cdiv(a->batch * a->heads_q * (int64_t)sq_pad * (D / 8), 256);
   PICO_LAUNCH(PICO_K_ATTN_BWD_PRE, "attn_bwd_pre", s,
               attn_bwd_pre_kernel<D><<<pre_blocks, 256, 0, s>>>(*a, delta, lse2, sq_pad));
@@ -814,10 +832,10 @@ int launch_bwd(const pico_attn_args* a, hipStream_t s) {
   }
   if (a->causal) {
     PICO_LAUNCH(PICO_K_ATTN_BWD_DQ, "attn_bwd_dq", s,
-                attn_bwd_dq_kernel<D, true><<<row_blocks, 256, 0, s>>>(*a, dq_part, slab, nkb, f32acc));
+                attn_bwd_dq_kernel<D, true><<<row_blocks, 256, 0, s>>>(*a, dq_part, slab, nkb, f32acc, rope_dk));
   } else {
     PICO_LAUNCH(PICO_K_ATTN_BWD_DQ, "attn_bwd_dq", s,
-                attn_bwd_dq_kernel<D, false><<<row_blocks, 256, 0, s>>>(*a, dq_part, slab, nkb, f32acc));
+                attn_bwd_dq_kernel<D, false><<<row_blocks, 256, 0, s>>>(*a, dq_part, slab, nkb, f32acc, rope_dk));
   }
   return 0;
 }
