@@ -84,6 +84,10 @@ int pico_prof_collect(int kernel_id, double* total_ms, int64_t* launches);
  * x, y: [rows, cols] bf16 row-major (row stride = cols); w: [cols] bf16; rstd: [rows] fp32 (saved
  * for backward). residual (optional, may be NULL): x_eff = bf16(x + residual), written to
  * residual_out when residual_out != NULL (layer_norm_fn(prenorm=True) semantics). */
+/* pico_rmsnorm_fwd that also writes y^T ([cols, rows], row stride ld_t): the x^T the next projection's
+ * weight-gradient GEMM reads. cols 1024 or 2048, rows multiple of 32, 16-byte aligned pointers. */
+int pico_rmsnorm_fwd_t(const void* x, const void* residual, const void* weight, void* y, void* residual_out,
+                       float* rstd, void* y_t, int64_t ld_t, int64_t rows, int64_t cols, float eps, void* stream);
 int pico_rmsnorm_fwd(const void* x, const void* residual, const void* weight, void* y,
                      void* residual_out, float* rstd, int64_t rows, int64_t cols, float eps,
                      void* stream);

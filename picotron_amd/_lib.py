@@ -54,6 +54,8 @@ _SIGNATURES = {
     "pico_prof_enable": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
     "pico_prof_collect": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(c_i64)]),
     "pico_rmsnorm_fwd": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, ctypes.c_float, c_vp]),
+    "pico_rmsnorm_fwd_t": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64,
+                                          ctypes.c_float, c_vp]),
     "pico_rmsnorm_bwd_workspace_bytes": (c_i64, [c_i64, c_i64]),
     "pico_rmsnorm_bwd": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp]),
     "pico_rmsnorm_bwd_acc": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.c_int, ctypes.c_float,

@@ -74,6 +74,91 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd_kernel(const bf16_t* __restri
   }
 }
 
+// Forward that also writes y^T ([cols, rows], row stride ldt): the x^T the following projection's
+// weight-gradient GEMM reads (TT form), at the cost of one extra write instead of a transpose pass.
+// One 512-thread workgroup per 32 rows (wave w: rows w, w + 8, ...; a lane owns 8 contiguous columns
+// per 512-column chunk as in rmsnorm_fwd_kernel); y is also staged into an LDS tile [32][cols + 8]
+// (128.5 KiB at cols = 2048), then each thread stores 8-token segments of y^T rows (4 x 16 B per
+// 64-B row segment). Requires cols == MAXC * 512 and rows % 32 == 0 (host checks).
+template <int MAXC, bool RES>
+__global__ __launch_bounds__(512) void rmsnorm_fwd_t_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
+                                                            const bf16_t* __restrict__ w, bf16_t* __restrict__ y,
+                                                            bf16_t* __restrict__ res_out, float* __restrict__ rstd,
+                                                            bf16_t* __restrict__ yt, int64_t ldt, float eps) {
+  constexpr int COLS = MAXC * 512, PITCH = COLS + 8;
+  extern __shared__ __attribute__((aligned(16))) unsigned short tile[];  // [32][PITCH]
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int64_t r0 = (int64_t)blockIdx.x * 32;
+  constexpr int RPW = 4;  // rows per wave (rows wid + 8 k): every load of the four rows issued first
+  u16x8 xr[RPW][MAXC], rr[RPW][MAXC];
+#pragma unroll
+  for (int k = 0; k < RPW; ++k) {
+    const int64_t row = r0 + wid + 8 * k;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      const int col = (c * 64 + lane) * 8;
+      xr[k][c] = *reinterpret_cast<const u16x8*>(x + row * COLS + col);
+      if constexpr (RES) rr[k][c] = *reinterpret_cast<const u16x8*>(res + row * COLS + col);
+    }
+  }
+  float ss[RPW];
+#pragma unroll
+  for (int k = 0; k < RPW; ++k) {
+    const int64_t row = r0 + wid + 8 * k;
+    ss[k] = 0.f;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      const int col = (c * 64 + lane) * 8;
+      if constexpr (RES) {
+        u16x8 sum;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) sum[j] = f2bf(bf2f(xr[k][c][j]) + bf2f(rr[k][c][j]));
+        xr[k][c] = sum;
+        if (res_out) *reinterpret_cast<u16x8*>(res_out + row * COLS + col) = sum;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float v = bf2f(xr[k][c][j]);
+        ss[k] += v * v;
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < RPW; ++k) ss[k] = wave_sum(ss[k]);
+#pragma unroll
+  for (int k = 0; k < RPW; ++k) {
+    const int lr = wid + 8 * k;
+    const int64_t row = r0 + lr;
+    const float rs = rsqrtf(ss[k] / (float)COLS + eps);
+    if (lane == 0) rstd[row] = rs;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      const int col = (c * 64 + lane) * 8;
+      float wf[8];
+      load8(w + col, wf);
+      u16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = f2bf(bf2f(xr[k][c][j]) * rs * wf[j]);
+      *reinterpret_cast<u16x8*>(y + row * COLS + col) = o;
+      *reinterpret_cast<u16x8*>(tile + lr * PITCH + col) = o;
+    }
+  }
+  __syncthreads();
+  // a task = 2 adjacent columns x 8 tokens: 8 dword LDS reads -> two 16-byte y^T segments
+  for (int task = threadIdx.x; task < COLS * 2; task += 512) {
+    const int cp = task >> 2, part = task & 3;
+    u16x8 o0, o1;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const unsigned v = *reinterpret_cast<const unsigned*>(tile + (8 * part + i) * PITCH + 2 * cp);
+      o0[i] = (unsigned short)(v & 0xffff);
+      o1[i] = (unsigned short)(v >> 16);
+    }
+    *reinterpret_cast<u16x8*>(yt + (int64_t)(2 * cp) * ldt + r0 + 8 * part) = o0;
+    *reinterpret_cast<u16x8*>(yt + (int64_t)(2 * cp + 1) * ldt + r0 + 8 * part) = o1;
+  }
+}
+
 // Backward: dx = rstd * (g - xhat * mean(g * xhat)), g = dy * w, xhat = x * rstd;
 // dw partial per workgroup (deterministic two-stage reduction, no atomics).
 // FULL: cols == MAXC * 512 (every lane chunk in range: no per-chunk predicates, which otherwise
@@ -229,6 +314,40 @@ int bwd_blocks(int64_t rows, int64_t cols) {  // one workgroup per CU at most: f
 }  // namespace
 
 extern "C" {
+
+int pico_rmsnorm_fwd_t(const void* x, const void* residual, const void* weight, void* y, void* residual_out,
+                       float* rstd, void* y_t, int64_t ld_t, int64_t rows, int64_t cols, float eps, void* stream) {
+  PICO_REQUIRE(x && weight && y && rstd && y_t, "pico_rmsnorm_fwd_t: null pointer");
+  PICO_REQUIRE(cols == 1024 || cols == 2048, "pico_rmsnorm_fwd_t: cols=%lld unsupported (1024 or 2048)",
+               (long long)cols);
+  PICO_REQUIRE(rows >= 0 && rows % 32 == 0 && ld_t >= rows && ld_t % 8 == 0,
+               "pico_rmsnorm_fwd_t: rows must be a multiple of 32 and ld_t >= rows, multiple of 8");
+  PICO_REQUIRE((((uintptr_t)x | (uintptr_t)y | (uintptr_t)y_t | (uintptr_t)weight | (uintptr_t)residual |
+                 (uintptr_t)residual_out) & 15) == 0,
+               "pico_rmsnorm_fwd_t: pointers must be 16-byte aligned");
+  PICO_REQUIRE(rows / 32 < (1ll << 31), "pico_rmsnorm_fwd_t: too many rows");
+  if (rows == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  const int nb = (int)(rows / 32);
+  const size_t lds = 32 * (cols + 8) * 2;
+  auto xp = (const bf16_t*)x;
+  auto rp = (const bf16_t*)residual;
+  auto wp = (const bf16_t*)weight;
+  auto go = [&](auto maxc, auto res) {
+    constexpr int M = decltype(maxc)::value;
+    constexpr bool R = decltype(res)::value;
+    auto k = rmsnorm_fwd_t_kernel<M, R>;
+    hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return pico_set_error("pico_rmsnorm_fwd_t: cannot set LDS size (%d)", (int)e);
+    PICO_LAUNCH(PICO_K_RMSNORM_FWD, "rmsnorm_fwd_t", s,
+                k<<<nb, 512, lds, s>>>(xp, rp, wp, (bf16_t*)y, (bf16_t*)residual_out, rstd, (bf16_t*)y_t, ld_t, eps));
+    return 0;
+  };
+  using I2 = std::integral_constant<int, 2>;
+  using I4 = std::integral_constant<int, 4>;
+  if (cols == 2048) return residual ? go(I4{}, std::true_type{}) : go(I4{}, std::false_type{});
+  return residual ? go(I2{}, std::true_type{}) : go(I2{}, std::false_type{});
+}
 
 int pico_rmsnorm_fwd(const void* x, const void* residual, const void* weight, void* y, void* residual_out,
                      float* rstd, int64_t rows, int64_t cols, float eps, void* stream) {

@@ -110,9 +110,11 @@ class RMSNorm(nn.Module):
 
     def forward(self, hidden_states, residual=None, dropout_p=0.0, prenorm=False, residual_in_fp32=False,
                 return_dropout_mask=False):
+        # the norm outputs of this model feed projections (qkv, gate|up, LM head) whose weight-gradient
+        # GEMM reads y^T: the kernel writes it alongside y (ops._wgrad_input picks it up)
         return ops.layer_norm_fn(hidden_states, self.weight, None, residual=residual, eps=self.eps,
                                  dropout_p=dropout_p, prenorm=prenorm, residual_in_fp32=residual_in_fp32,
-                                 is_rms_norm=True, return_dropout_mask=return_dropout_mask)
+                                 is_rms_norm=True, return_dropout_mask=return_dropout_mask, _emit_transposed=True)
 
 
 TritonRMSNorm = RMSNorm

@@ -40,7 +40,7 @@ def _need(t, name, dtype=_BF16):
 # --------------------------------------------------------------------------------------------
 class _RMSNormFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, residual, weight, eps, prenorm):
+    def forward(ctx, x, residual, weight, eps, prenorm, want_t=False):
         _need(x, "x")
         _need(weight, "weight")
         shape = x.shape
@@ -57,8 +57,18 @@ class _RMSNormFn(torch.autograd.Function):
             res2 = residual.reshape(-1, cols).contiguous()
             res_out = torch.empty_like(x2)
         w = weight.contiguous()
-        _lib.check(lib.pico_rmsnorm_fwd(_lib.ptr(x2), _lib.ptr(res2), _lib.ptr(w), _lib.ptr(y), _lib.ptr(res_out),
-                                        _lib.ptr(rstd), rows, cols, float(eps), _lib.stream_of(x)), "pico_rmsnorm_fwd")
+        yt = None
+        if want_t and os.getenv("PICO_XT_WGRAD", "1") != "0" and cols in (1024, 2048) and rows % 32 == 0 and \
+                all(t is None or t.data_ptr() % 16 == 0 for t in (x2, res2, w)):
+            # y^T as a by-product for the next projection's TT wgrad GEMM (no separate transpose pass)
+            yt = torch.empty((cols, rows), dtype=x.dtype, device=x.device)
+            _lib.check(lib.pico_rmsnorm_fwd_t(_lib.ptr(x2), _lib.ptr(res2), _lib.ptr(w), _lib.ptr(y), _lib.ptr(res_out),
+                                              _lib.ptr(rstd), _lib.ptr(yt), rows, rows, cols, float(eps),
+                                              _lib.stream_of(x)), "pico_rmsnorm_fwd_t")
+        else:
+            _lib.check(lib.pico_rmsnorm_fwd(_lib.ptr(x2), _lib.ptr(res2), _lib.ptr(w), _lib.ptr(y), _lib.ptr(res_out),
+                                            _lib.ptr(rstd), rows, cols, float(eps), _lib.stream_of(x)),
+                       "pico_rmsnorm_fwd")
         x_eff = res_out if res_out is not None else x2
         ctx.save_for_backward(x_eff, w, rstd)
         ctx.weight_param = weight if weight.requires_grad else None
@@ -66,6 +76,8 @@ class _RMSNormFn(torch.autograd.Function):
         ctx.has_residual = residual is not None
         ctx.prenorm = prenorm
         y = y.view(shape)
+        if yt is not None:
+            y._pico_t = yt
         if prenorm:
             return y, (res_out if res_out is not None else x2).view(shape)
         return y
@@ -90,7 +102,7 @@ class _RMSNormFn(torch.autograd.Function):
         if ready is not None:
             ready()
         dx = dx.view(ctx.shape)
-        return dx, (dx if ctx.has_residual else None), dw, None, None
+        return dx, (dx if ctx.has_residual else None), dw, None, None, None
 
 
 def _norm_grad_target(p, w):
@@ -118,7 +130,7 @@ def rms_norm(x, weight, eps=1e-5, residual=None, prenorm=False):
 
 def layer_norm_fn(x, weight, bias, residual=None, x1=None, weight1=None, bias1=None, eps=1e-6, dropout_p=0.0,
                   rowscale=None, prenorm=False, residual_in_fp32=False, is_rms_norm=False,
-                  return_dropout_mask=False):
+                  return_dropout_mask=False, _emit_transposed=False):
     """flash-attn 2.5 `layer_norm_fn` restricted to what picotron calls: RMS norm, no bias/dropout
     (ref picotron/model.py:53-64). Returns y, or (y, residual_out) when prenorm=True."""
     if not is_rms_norm:
@@ -129,7 +141,7 @@ def layer_norm_fn(x, weight, bias, residual=None, x1=None, weight1=None, bias1=N
         raise NotImplementedError("picotron_amd.layer_norm_fn: dropout unsupported")
     if residual_in_fp32:
         raise NotImplementedError("picotron_amd.layer_norm_fn: residual_in_fp32 unsupported")
-    return _RMSNormFn.apply(x, residual, weight, eps, prenorm)
+    return _RMSNormFn.apply(x, residual, weight, eps, prenorm, bool(_emit_transposed))
 
 
 # --------------------------------------------------------------------------------------------
@@ -572,7 +584,7 @@ class _GateUpSwiGLUFn(torch.autograd.Function):
                                                      2 * I, I, T, _lib.stream_of(gu)), "pico_swiglu_fwd_t")
         else:
             _swiglu_fwd(gu, gu[:, I:], h, T, I, 2 * I, I)
-        ctx.save_for_backward(_wgrad_input(x2, 2 * I), gu, W)
+        ctx.save_for_backward(_wgrad_input(x2, 2 * I, x), gu, W)
         ctx.params = (w_gate, w_up)
         ctx.xshape = x.shape
         out = h.view(*x.shape[:-1], I)
@@ -737,7 +749,7 @@ class _QKVRopeAttentionFn(torch.autograd.Function):
         o_t = torch.empty((nh * D, B * S), dtype=x.dtype, device=x.device) \
             if os.getenv("PICO_XT_WGRAD", "1") != "0" else None
         o, lse = attention_block_fwd(q, k, v, scale, causal, o_t=o_t)
-        ctx.save_for_backward(_wgrad_input(x2, N), W, qkv, o, lse, cos, sin)
+        ctx.save_for_backward(_wgrad_input(x2, N, x), W, qkv, o, lse, cos, sin)
         ctx.params = (wq, wk, wv)
         ctx.meta = (B, S, Hd, nh, nkv, D, causal, scale)
         out = o.view(B, S, nh * D)

@@ -41,8 +41,12 @@ def main(iters=50):
         y, res = ops.rms_norm(x, w, 1e-5, residual=r, prenorm=True)
         torch.autograd.backward([y, res], [torch.ones_like(y), torch.ones_like(res)])
 
+    def run_norm_t():
+        ops._RMSNormFn.apply(x.detach(), r.detach(), w.detach(), 1e-5, True, True)
+
     cases = [
         ("rmsnorm", run_norm, [L.K_RMSNORM_FWD, L.K_RMSNORM_BWD, L.K_RMSNORM_DW]),
+        ("rmsnorm_t", run_norm_t, [L.K_RMSNORM_FWD]),
         ("rope", lambda: ops._rope_launch(qkv[:, :, :2 * NH], qkv[:, :, :2 * NH], cos, sin, False), [L.K_ROPE]),
         ("swiglu", lambda: (ops._swiglu_fwd(gu, gu[:, I:], h, T, I, 2 * I, I),
                             ops._swiglu_bwd(dh, gu, gu[:, I:], dgu, dgu[:, I:], T, I, 2 * I, I)),
@@ -69,7 +73,7 @@ def main(iters=50):
         for k in kids:
             ms, n = L.prof_collect(k)
             us = 1e3 * ms / max(n, 1)
-            out = {"kernel": L.KERNEL_NAMES[k] + ("" if k != L.K_TRANSPOSE else ":" + name), "avg_us": round(us, 2), "launches": n}
+            out = {"kernel": L.KERNEL_NAMES[k] + ("" if k not in (L.K_TRANSPOSE,) and name != "rmsnorm_t" else ":" + name), "avg_us": round(us, 2), "launches": n}
             if k in work:
                 out["GB_s"] = round(work[k] / (us * 1e-6) / 1e9, 1)
                 out["frac_of_8TBs"] = round(out["GB_s"] / 8000, 3)

@@ -521,3 +521,20 @@ def test_swiglu_fwd_transposed_output():
     assert torch.equal(h, h_ref)
     assert torch.equal(ht[:, :T], h.t())
     assert bool((ht[:, T:] == 2.0).all())
+
+
+@pytest.mark.parametrize("rows,cols,res", [(64, 2048, True), (96, 1024, False), (4096, 2048, True)])
+def test_rmsnorm_fwd_transposed_output(rows, cols, res):
+    """pico_rmsnorm_fwd_t == pico_rmsnorm_fwd bit for bit (y, residual_out, rstd) and writes y^T exactly."""
+    from picotron_amd import ops
+    torch.manual_seed(rows + cols)
+    x = torch.randn(rows, cols, dtype=BF, device=DEV)
+    r = torch.randn(rows, cols, dtype=BF, device=DEV) if res else None
+    w = (1 + 0.1 * torch.randn(cols, device=DEV)).to(BF)
+    out_ref = ops._RMSNormFn.apply(x, r, w, 1e-5, res, False)
+    out = ops._RMSNormFn.apply(x, r, w, 1e-5, res, True)
+    y_ref, y = (out_ref[0], out[0]) if res else (out_ref, out)
+    assert torch.equal(y, y_ref)
+    if res:
+        assert torch.equal(out[1], out_ref[1])
+    assert torch.equal(y._pico_t, y.t())
