@@ -68,17 +68,19 @@ def kernel_work(kid, cfg, mbs, seq):
     table = {
         L.K_ATTN_FWD: (attn_fwd, "flop", "mfma"),
         L.K_ATTN_BWD: (2.5 * attn_fwd, "flop", "mfma"),
-        # residual-fused form (29 of 31 launches): fwd reads x, residual, writes y, residual_out;
-        # bwd reads dy, d(residual_out), x, writes dx (+4 B/row rstd, small dw partials)
-        L.K_RMSNORM_FWD: (4 * T * Hd * 2 + 4 * T, "byte", "hbm"),
+        # residual-fused form (29 of 31 launches): fwd reads x, residual, writes y, residual_out and y^T
+        # (the next projection's wgrad input); bwd reads dy, d(residual_out), x, writes dx (+4 B/row
+        # rstd, small dw partials)
+        L.K_RMSNORM_FWD: (5 * T * Hd * 2 + 4 * T, "byte", "hbm"),
         L.K_RMSNORM_BWD: (4 * T * Hd * 2 + 4 * T, "byte", "hbm"),
         L.K_ROPE: (2 * T * (H + Hkv) * D * 2, "byte", "hbm"),  # q|k heads in one launch, read + write
-        L.K_SWIGLU_FWD: (3 * T * I * 2, "byte", "hbm"),
+        L.K_SWIGLU_FWD: (4 * T * I * 2, "byte", "hbm"),  # g, u read; h and h^T written
         L.K_SWIGLU_BWD: (5 * T * I * 2, "byte", "hbm"),
         # reads O, dO, LSE; writes delta and LSE*log2(e) (fp32 per query row and head)
         L.K_ATTN_BWD_PRE: (2 * T * Hd * 2 + 3 * T * H * 4, "byte", "hbm"),
-        # reads the fp32 dQ partial slabs of the key blocks at or before each query row, writes bf16 dQ
-        L.K_ATTN_BWD_DQ: (dq_slabs * T * Hd * 4 + T * Hd * 2, "byte", "hbm"),
+        # reads the fp32 dQ partial slabs of the key blocks at or before each query row, writes bf16 dQ;
+        # RoPE^-1 of dK in place in the same launch (read + write)
+        L.K_ATTN_BWD_DQ: (dq_slabs * T * Hd * 4 + T * Hd * 2 + 2 * T * Hkv * D * 2, "byte", "hbm"),
     }
     return table.get(kid)
 
