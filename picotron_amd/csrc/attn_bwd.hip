@@ -186,8 +186,11 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(const pico_attn_args 
   float s = 0.f;
 #pragma unroll
   for (int j = 0; j < 8; ++j) s += bf2f(ov[j]) * bf2f(dv[j]);
-#pragma unroll
-  for (int o = LPR / 2; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
+  // sum over the LPR (8 or 16) lanes of the row: DPP quad swaps + half-row mirror (+ row mirror)
+  s += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(s), 0xB1, 0xF, 0xF, false));
+  s += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(s), 0x4E, 0xF, 0xF, false));
+  s += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(s), 0x141, 0xF, 0xF, false));
+  if constexpr (LPR == 16) s += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(s), 0x140, 0xF, 0xF, false));
   if (sub == 0) {
     delta[row] = -s;  // negated: it initialises the dP accumulator (dP - delta in the MFMA chain)
     lse2[row] = a.lse[bh * a.seqlen_q + q] * LOG2E;

@@ -16,12 +16,19 @@
 
 namespace {
 
+PICO_DEV float wave_max_dpp(float v) {
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false)));
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false)));
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, false)));
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140, 0xF, 0xF, false)));
+  const auto r16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = fmaxf(__uint_as_float(r16[0]), __uint_as_float(r16[1]));
+  const auto r32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r32[0]), __uint_as_float(r32[1]));
+}
+
 PICO_DEV float block_reduce(float v, float* red, bool is_max) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) {
-    const float u = __shfl_xor(v, o, 64);
-    v = is_max ? fmaxf(v, u) : v + u;
-  }
+  v = is_max ? wave_max_dpp(v) : wave_sum_dpp(v);  // DPP / permlane, no LDS round trips
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   __syncthreads();
   if (lane == 0) red[wid] = v;
@@ -58,7 +65,7 @@ __global__ __launch_bounds__(256) void ce_fwd_kernel(const bf16_t* __restrict__ 
     const int ch = threadIdx.x + 256 * c;
     if (ch < nchunk) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) s += __expf(bf2f(v[c][j]) - m);
+      for (int j = 0; j < 8; ++j) s += __builtin_amdgcn_exp2f((bf2f(v[c][j]) - m) * 1.4426950408889634f);
     }
   }
   s = block_reduce(s, red, false);
