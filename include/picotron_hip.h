@@ -204,6 +204,12 @@ int pico_embedding_bwd(const int64_t* sorted_ids, const int64_t* sorted_pos, con
  *      ignored targets); grad_scale is a DEVICE fp32 scalar (grad_out / n_valid), row stride ldd. */
 int pico_cross_entropy_fwd(const void* logits, int64_t ld, const int64_t* target, float* lse, float* loss,
                            int64_t rows, int64_t vocab, int64_t ignore_index, void* stream);
+/* fused forward + gradient: as pico_cross_entropy_fwd, and the logits are overwritten IN PLACE with
+ * (softmax - onehot) * (*grad_scale) (device fp32 scalar; 0 rows for ignored targets) — the gradient of
+ * mean CE for a unit upstream gradient, which the caller scales after the LM-head GEMMs. */
+int pico_cross_entropy_fwd_grad(void* logits, int64_t ld, const int64_t* target, float* lse, float* loss,
+                                const float* grad_scale, int64_t rows, int64_t vocab, int64_t ignore_index,
+                                void* stream);
 int pico_cross_entropy_bwd(const void* logits, int64_t ld, const int64_t* target, const float* lse,
                            const float* grad_scale, void* dlogits, int64_t ldd, int64_t rows, int64_t vocab,
                            int64_t ignore_index, void* stream);

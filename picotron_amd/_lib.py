@@ -76,6 +76,7 @@ _SIGNATURES = {
     "pico_cast_f32_bf16": (ctypes.c_int, [c_vp, c_vp, c_i64, c_vp]),
     "pico_embedding_bwd": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, ctypes.c_int, ctypes.c_float, c_vp]),
     "pico_cross_entropy_fwd": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp]),
+    "pico_cross_entropy_fwd_grad": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp]),
     "pico_cross_entropy_bwd": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp]),
     "pico_transpose_bf16": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_i64, c_i64, c_vp]),
 }

@@ -107,6 +107,66 @@ __global__ __launch_bounds__(256) void ce_bwd_kernel(const bf16_t* __restrict__ 
   }
 }
 
+// Forward that also produces the gradient in place: lse, loss as ce_fwd_kernel, then the row (still in
+// registers) is overwritten with dlogits = (softmax - onehot(t)) * (*gscale) (0 for ignored rows). One
+// read + one write of the logits instead of fwd read + bwd read + bwd write; the caller applies the
+// upstream gradient later (it scales the LM-head GEMMs' results, not the logits).
+template <int NCH>
+__global__ __launch_bounds__(256) void ce_fwd_grad_kernel(bf16_t* __restrict__ logits, int64_t ld,
+                                                          const int64_t* __restrict__ target, float* __restrict__ lse,
+                                                          float* __restrict__ loss, const float* __restrict__ gscale,
+                                                          int vocab, int64_t ignore) {
+  __shared__ float red[4];
+  const int64_t row = blockIdx.x;
+  bf16_t* x = logits + row * ld;
+  const int nchunk = vocab / 8;
+  const int64_t t = target[row];
+  const bool skip = t == ignore || t < 0 || t >= vocab;
+  const float xt = skip ? 0.f : bf2f(x[skip ? 0 : t]);  // read before the row is overwritten
+  u16x8 v[NCH];
+  float m = -INFINITY;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int ch = threadIdx.x + 256 * c;
+    if (ch < nchunk) {
+      v[c] = *reinterpret_cast<const u16x8*>(x + 8 * ch);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) m = fmaxf(m, bf2f(v[c][j]));
+    }
+  }
+  m = block_reduce(m, red, true);
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int ch = threadIdx.x + 256 * c;
+    if (ch < nchunk) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += __builtin_amdgcn_exp2f((bf2f(v[c][j]) - m) * 1.4426950408889634f);
+    }
+  }
+  s = block_reduce(s, red, false);
+  const float l = m + __logf(s);
+  if (threadIdx.x == 0) {
+    lse[row] = l;
+    loss[row] = skip ? 0.f : l - xt;
+  }
+  const float g = skip ? 0.f : *gscale;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int ch = threadIdx.x + 256 * c;
+    if (ch < nchunk) {
+      u16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float p = __builtin_amdgcn_exp2f((bf2f(v[c][j]) - l) * 1.4426950408889634f);
+        if (8 * ch + j == t) p -= 1.f;
+        o[j] = f2bf(p * g);
+      }
+      *reinterpret_cast<u16x8*>(x + 8 * ch) = o;
+    }
+  }
+}
+
 int nch_for(int64_t vocab) {
   const int64_t per = (vocab / 8 + 255) / 256;
   for (int n : {4, 8, 16, 24, 32, 48, 64})
@@ -140,6 +200,23 @@ extern "C" int pico_cross_entropy_fwd(const void* logits, int64_t ld, const int6
   CE_SWITCH(nch, PICO_LAUNCH(PICO_K_CE_FWD, "cross_entropy_fwd", s,
                              ce_fwd_kernel<N><<<(int)rows, 256, 0, s>>>((const bf16_t*)logits, ld, target, lse, loss,
                                                                         (int)vocab, ignore_index)))
+  return 0;
+}
+
+extern "C" int pico_cross_entropy_fwd_grad(void* logits, int64_t ld, const int64_t* target, float* lse, float* loss,
+                                           const float* grad_scale, int64_t rows, int64_t vocab, int64_t ignore_index,
+                                           void* stream) {
+  PICO_REQUIRE(rows >= 0 && vocab > 0 && vocab % 8 == 0 && ld % 8 == 0 && ld >= vocab,
+               "pico_cross_entropy_fwd_grad: vocab (%lld) and row stride must be multiples of 8", (long long)vocab);
+  const int nch = nch_for(vocab);
+  PICO_REQUIRE(nch > 0, "pico_cross_entropy_fwd_grad: vocab %lld too large", (long long)vocab);
+  PICO_REQUIRE(rows < (1ll << 31), "pico_cross_entropy_fwd_grad: too many rows");
+  if (rows == 0) return 0;
+  PICO_REQUIRE(logits && target && lse && loss && grad_scale, "pico_cross_entropy_fwd_grad: null pointer");
+  hipStream_t s = (hipStream_t)stream;
+  CE_SWITCH(nch, PICO_LAUNCH(PICO_K_CE_FWD, "cross_entropy_fwd_grad", s,
+                             ce_fwd_grad_kernel<N><<<(int)rows, 256, 0, s>>>((bf16_t*)logits, ld, target, lse, loss,
+                                                                             grad_scale, (int)vocab, ignore_index)))
   return 0;
 }
 

@@ -286,7 +286,9 @@ class Llama(nn.Module):
         # NB: the reference never re-initialises final_proj here (ref :262 lacks the call); it is
         # zero-initialised by init_model_with_materialized_weights (ref picotron/checkpoint.py:88-91).
 
-    def forward(self, input_ids, attention_mask=None, position_ids: torch.Tensor = None):
+    def forward(self, input_ids, attention_mask=None, position_ids: torch.Tensor = None, return_hidden=False):
+        """Logits [B, S, V] (ref :264-271); return_hidden=True stops after the final norm (the fused LM
+        head + cross-entropy of train._micro_batch consumes it)."""
         x = self.embedding(input_ids)
         if os.getenv("PICO_UNFUSED", "0") == "1":
             for layer in self.decoder_layers:
@@ -295,9 +297,10 @@ class Llama(nn.Module):
         delta, residual = x, None
         for layer in self.decoder_layers:
             delta, residual = layer.forward_fused(delta, residual)
-        if residual is None:
-            return _proj(self.final_proj, self.final_norm(delta))
-        return _proj(self.final_proj, self.final_norm(delta, residual=residual))
+        h = self.final_norm(delta) if residual is None else self.final_norm(delta, residual=residual)
+        if return_hidden:
+            return h
+        return _proj(self.final_proj, h)
 
 
 def build_llama(config, device="cuda", dtype=torch.bfloat16):

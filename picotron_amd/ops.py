@@ -492,6 +492,62 @@ class _CrossEntropyFn(torch.autograd.Function):
         return dlogits, None, None
 
 
+class _LMHeadCEFn(torch.autograd.Function):
+    """mean F.cross_entropy(x W^T, target) in one autograd node — the LM head (ref picotron/model.py:246,
+    269) and the loss (ref train.py:46-49) fused: the logits [T, V] are produced by one GEMM into a buffer
+    that the CE kernel turns, in the same read, into the loss statistics AND dlogits for a unit upstream
+    gradient (in place, one write). The backward only runs the two LM-head GEMMs on it, scaling their
+    results by the actual upstream gradient g: dx = g (dlogits W), dW += dlogits^T (g x) — exact for any
+    g (a device scalar; no host sync). Logits are never materialised twice and never re-read by a CE
+    backward."""
+
+    @staticmethod
+    def forward(ctx, x, w, target, ignore_index):
+        _need(x, "x")
+        _need(w, "w")
+        H = x.shape[-1]
+        x2 = x.reshape(-1, H)
+        T, V = x2.shape[0], w.shape[0]
+        logits = torch.nn.functional.linear(x2, w)  # [T, V] bf16, becomes dlogits in place below
+        t = target.reshape(-1)
+        if t.dtype != torch.int64:
+            t = t.long()
+        t = t.contiguous()
+        n_valid = (t != ignore_index).sum().to(torch.float32)
+        gscale = (1.0 / n_valid).reshape(1)
+        lse = torch.empty(T, dtype=torch.float32, device=x.device)
+        loss_rows = torch.empty(T, dtype=torch.float32, device=x.device)
+        _lib.check(_lib.load().pico_cross_entropy_fwd_grad(_lib.ptr(logits), logits.stride(0), _lib.ptr(t),
+                                                           _lib.ptr(lse), _lib.ptr(loss_rows), _lib.ptr(gscale), T, V,
+                                                           int(ignore_index), _lib.stream_of(x)),
+                   "pico_cross_entropy_fwd_grad")
+        loss = loss_rows.sum() / n_valid
+        ctx.save_for_backward(logits, _wgrad_input(x2, V, x), w)
+        ctx.xshape = x.shape
+        return loss.to(x.dtype)
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        dlogits, xin, w = ctx.saved_tensors
+        g = grad_out.to(torch.float32)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = dgrad(dlogits, w, (w,))
+            dx.mul_(g)
+            dx = dx.view(ctx.xshape)
+        dw = None
+        if ctx.needs_input_grad[1]:
+            # scale the small GEMM input instead of dlogits: dW = dlogits^T (g x) (layout of x^T kept;
+            # exact when g is a power of two, e.g. 1 / grad_acc)
+            dw = wgrad_accumulate((w,), dlogits, xin * g)[0]
+        return dx, dw, None, None
+
+
+def lm_head_cross_entropy(x, w, target, ignore_index=-100):
+    """mean cross-entropy of the LM head x W^T against target, fused (_LMHeadCEFn)."""
+    return _LMHeadCEFn.apply(x, w, target, ignore_index)
+
+
 def cross_entropy(logits, target, ignore_index=-100, reduction="mean"):
     """F.cross_entropy for [N, V] bf16 logits on a HIP device (mean reduction)."""
     if reduction != "mean":

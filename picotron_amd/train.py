@@ -23,11 +23,32 @@ def _cross_entropy(outputs, targets):
     return F.cross_entropy(outputs, targets, reduction="mean")
 
 
+def _fused_lm_head(model):
+    """The LM head of `model` (or of the module a DP wrapper holds) when the fused LM head + CE applies:
+    our Llama (forward(return_hidden=True)), a bias-free nn.Linear head, bf16 on a HIP device."""
+    core = getattr(model, "module", model)
+    head = getattr(core, "final_proj", None)
+    if os.getenv("PICO_UNFUSED", "0") == "1" or os.getenv("PICO_FUSED_LM_CE", "1") == "0":
+        return None
+    if not hasattr(core, "decoder_layers") or type(head) is not torch.nn.Linear or head.bias is not None:
+        return None
+    w = head.weight
+    if not w.is_cuda or w.dtype != torch.bfloat16 or w.shape[0] % 8 != 0:
+        return None
+    return head
+
+
 def _micro_batch(model, input_ids, target_ids, grad_acc_steps):
-    outputs = model(input_ids=input_ids)
-    batch_size, seq_len = input_ids.shape
-    outputs = outputs.view(seq_len * batch_size, -1)
-    loss = _cross_entropy(outputs, target_ids.reshape(-1)) / grad_acc_steps
+    head = _fused_lm_head(model)
+    if head is not None:  # fused LM head + cross-entropy (SURVEY §8f row 1): logits never re-read
+        from . import ops
+        h = model(input_ids=input_ids, return_hidden=True)
+        loss = ops.lm_head_cross_entropy(h, head.weight, target_ids.reshape(-1)) / grad_acc_steps
+    else:
+        outputs = model(input_ids=input_ids)
+        batch_size, seq_len = input_ids.shape
+        outputs = outputs.view(seq_len * batch_size, -1)
+        loss = _cross_entropy(outputs, target_ids.reshape(-1)) / grad_acc_steps
     loss.backward()
     return loss.detach()
 

@@ -43,7 +43,7 @@ def main():
         print(json.dumps(r), flush=True)
 
 
-if __name__ == "__main__" and "--wgrad" not in __import__("sys").argv:
+if __name__ == "__main__" and "--wgrad" not in __import__("sys").argv and "--fwd" not in __import__("sys").argv:
     main()
 
 
@@ -70,3 +70,21 @@ def wgrad_main():
 
 if __name__ == "__main__" and "--wgrad" in __import__("sys").argv:
     wgrad_main()
+
+
+def fwd_main():
+    """forward y = x W^T with x given row-major (NT) vs as a transposed view of x^T [K, T] (TT)."""
+    torch.manual_seed(0)
+    for name in ("qkv", "gate_up", "lm_head", "o", "down"):
+        N, K = SHAPES[name]
+        x = torch.randn(T, K, device="cuda", dtype=torch.bfloat16)
+        xt = x.t().contiguous()
+        w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.02
+        r = {"shape": name, "N": N, "K": K}
+        r["fwd_NT"] = bench(lambda: F.linear(x, w))
+        r["fwd_from_xt"] = bench(lambda: torch.matmul(xt.t(), w.t()))
+        print(json.dumps(r), flush=True)
+
+
+if __name__ == "__main__" and "--fwd" in __import__("sys").argv:
+    fwd_main()

@@ -443,6 +443,41 @@ def test_cross_entropy_matches_torch(V, ignore):
     assert abs(float(t_loss) - float(loss)) <= 1.6e-2 * abs(float(ref)) + 2e-3
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("V,ignore,g", [(4000, False, 1.0), (4000, True, 0.25), (49152, True, 1.0 / 3)])
+def test_lm_head_cross_entropy_fused(V, ignore, g):
+    """ops.lm_head_cross_entropy (LM head GEMM + CE with dlogits written in the forward pass) ==
+    mean F.cross_entropy(x W^T) in fp64: loss, dx and dW (accumulated onto an existing .grad) for a
+    non-unit upstream gradient g, ignore_index rows excluded; and it agrees with the unfused
+    ops.linear + ops.cross_entropy path."""
+    from picotron_amd import ops
+    torch.manual_seed(V + int(ignore))
+    T, H = 512, 256
+    x = (torch.randn(T, H, device=DEV) * 0.5).to(BF).requires_grad_(True)
+    w = (torch.randn(V, H, device=DEV) * 0.05).to(BF).requires_grad_(True)
+    w0 = (torch.randn(V, H, device=DEV) * 1e-5).to(BF)  # same scale as dW: accumulation visible in bf16
+    w.grad = w0.clone()
+    tgt = torch.randint(0, V, (T,), device=DEV)
+    if ignore:
+        tgt[::5] = -100
+    loss = ops.lm_head_cross_entropy(x, w, tgt)
+    (loss * g).backward()
+    xd, wd = x.detach().double().requires_grad_(True), w.detach().double().requires_grad_(True)
+    ref = torch.nn.functional.cross_entropy(xd @ wd.t(), tgt)
+    (ref * g).backward()
+    assert loss.dtype == BF
+    assert abs(float(loss) - float(ref)) <= 8e-3 * abs(float(ref)) + 1e-3
+    assert rel_l2(x.grad.cpu(), xd.grad.cpu()) < 1.5e-2
+    assert rel_l2((w.grad.double() - w0.double()).cpu(), wd.grad.cpu()) < 3e-2
+    # the unfused path on the same inputs
+    x2 = x.detach().clone().requires_grad_(True)
+    w2 = w.detach().clone().requires_grad_(True)
+    l2 = ops.cross_entropy(ops.linear(x2, w2), tgt)
+    (l2 * g).backward()
+    assert abs(float(l2) - float(loss)) <= 1e-2 * abs(float(ref)) + 2e-3
+    assert rel_l2(x.grad.cpu(), x2.grad.cpu()) < 1.5e-2
+
+
 # ------------------------------------------------------------------------------------------ transpose
 @pytest.mark.parametrize("R,C,ld_pad", [(4096, 2048, 0), (6144, 2048, 0), (2048, 49152, 0), (72, 8, 0),
                                         (8, 136, 0), (200, 264, 16), (64, 64, 8)])

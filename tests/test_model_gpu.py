@@ -157,6 +157,31 @@ def test_fused_paths_match_unfused(golden_loss, monkeypatch):
         assert rel_l2(outs["0"][1][n].cpu(), outs["1"][1][n].cpu()) < 3e-2, n
 
 
+def test_micro_batch_fused_lm_head_ce(golden_loss, monkeypatch):
+    """train._micro_batch with the fused LM head + cross-entropy == the logits + CE path (loss and every
+    parameter's accumulated gradient, 2 micro-batches of grad_acc 2, within bf16 tolerance)."""
+    from picotron_amd import train
+    from picotron_amd.model import build_llama
+    from conftest import rel_l2
+    cfg = _cfg(golden_loss)
+    g = torch.Generator("cuda").manual_seed(17)
+    toks = [torch.randint(0, cfg.vocab_size, (2, 129), device="cuda", generator=g) for _ in range(2)]
+    outs = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("PICO_FUSED_LM_CE", mode)
+        torch.manual_seed(7)
+        m = build_llama(cfg, "cuda", BF)
+        with torch.no_grad():
+            m.final_proj.weight.normal_(0, 0.02, generator=torch.Generator("cuda").manual_seed(1))
+        assert (train._fused_lm_head(m) is not None) == (mode == "1")
+        losses = [train._micro_batch(m, t[:, :-1], t[:, 1:], 2) for t in toks]
+        torch.cuda.synchronize()
+        outs[mode] = (sum(float(l) for l in losses), {n: p.grad.float().clone() for n, p in m.named_parameters()})
+    assert abs(outs["1"][0] - outs["0"][0]) <= 1e-2 * abs(outs["0"][0])
+    for n in outs["0"][1]:
+        assert rel_l2(outs["1"][1][n].cpu(), outs["0"][1][n].cpu()) < 3e-2, n
+
+
 def _train_grads(cfg, toks, fusion, monkeypatch, dp=None):
     """grad_acc = len(toks) micro-batches; returns {name: fp32 grad (or main_grad with DP)}."""
     from picotron_amd.model import build_llama
