@@ -45,6 +45,15 @@
 #ifndef PICO_BWD_STAGGER
 #define PICO_BWD_STAGGER 1
 #endif
+//   PICO_BWD_GROUP_D64: query tiles per workgroup barrier for D = 64 (the ring holds two groups; 2G dS^T
+//     images). D = 128 keeps 1 (its LDS has no room for more dS images)
+#ifndef PICO_BWD_GROUP_D64
+#define PICO_BWD_GROUP_D64 2
+#endif
+//   PICO_BWD_GROUP_UNROLL: unroll factor of the loop over a group's tiles (1: one copy of the tile code)
+#ifndef PICO_BWD_GROUP_UNROLL
+#define PICO_BWD_GROUP_UNROLL 1
+#endif
 
 namespace {
 
@@ -63,10 +72,12 @@ struct BwdCfg {
   static constexpr int LSD = 1024;              // LSE*log2e [32] | delta [32] (one DMA piece)
   static constexpr int SLOT = 2 * QIMG + LSD;
   static constexpr int KIMG = BK * RB;
-  static constexpr int DSIMG = BK * BQ * 2;     // dS^T [key][q] bf16, 64-B rows (two: tiles t, t-1)
+  static constexpr int DSIMG = BK * BQ * 2;     // dS^T [key][q] bf16, 64-B rows (2G: this group's, the last)
+  static constexpr int G = D == 64 ? PICO_BWD_GROUP_D64 : 1;  // tiles per barrier
   static constexpr int NBUF = D == 64 ? 4 : 3;  // ring slots
-  static constexpr int PD = NBUF - 1;           // prefetch distance (tiles)
-  static constexpr int SMEM = KIMG + NBUF * SLOT + 2 * DSIMG;
+  static constexpr int PD = NBUF - G;           // prefetch distance (tiles)
+  static constexpr int SMEM = KIMG + NBUF * SLOT + 2 * G * DSIMG;
+  static_assert(PD >= 1, "ring too small for the group");
   static constexpr int RPP = 1024 / RB;         // image rows per 1-KiB DMA piece
   static constexpr int NQP = QIMG / 1024;       // pieces per Q (or dO) tile
   static constexpr int NP = 2 * NQP + 1;        // pieces per tile
@@ -210,7 +221,7 @@ __global__ __launch_bounds__(BwdCfg<D>::NTH, bwd_waves_per_eu<D>()) void attn_bw
   __shared__ __attribute__((aligned(16))) char smem[C::SMEM];
   char* kimg = smem;
   char* ring = smem + C::KIMG;
-  char* dsimg0 = smem + C::KIMG + C::NBUF * C::SLOT;  // dS^T [key][q] images of tiles t (t % 2), t - 1
+  char* dsimg0 = smem + C::KIMG + C::NBUF * C::SLOT;  // dS^T [key][q] images: group u's tiles at (u % 2) G + j
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (scalar branches)
@@ -550,52 +561,118 @@ __global__ __launch_bounds__(BwdCfg<D>::NTH, bwd_waves_per_eu<D>()) void attn_bw
     }
   };
 
-  // One barrier per tile: iteration t computes tile t (S/dP -> P/dS -> dV/dK, dS image t % 2) and the
-  // dQ tile of t-1, whose dS image the barrier published. The two waves sharing a SIMD (w, w + 4) run
-  // them in opposite orders, so one's S/dP and dV/dK MFMAs overlap the other's LDS-latency-bound dQ
-  // steps and softmax VALU instead of both waves contending for the same unit in lockstep.
-  // Per-wave vector-memory ops in issue order, iteration j: DMA pieces of tile j+PD, dQ stores of j-1.
+  // One barrier per group of G tiles: group u computes its tiles (S/dP -> P/dS -> dV/dK, dS images
+  // (u % 2) G + j) and the dQ tiles of group u - 1, whose dS images the barrier published. The two
+  // waves sharing a SIMD (w, w + 4) run them in opposite orders, so one's S/dP and dV/dK MFMAs overlap
+  // the other's LDS-latency-bound dQ steps and softmax VALU instead of both waves contending for the
+  // same unit in lockstep. The ring holds the tiles of groups u and u + 1 ... (PD = NBUF - G ahead):
+  // group u issues the DMA of tiles uG + PD .. uG + PD + G - 1, whose slots held tiles of group u - 1
+  // or earlier (retired before the barrier).
+  // Per-wave vector-memory ops in issue order, group g: DMA pieces of its G look-ahead tiles, then the
+  // dQ stores of group g - 1.
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();  // K image and the prologue tiles visible
+  constexpr int GT = C::G, PD = C::PD;  // tiles per barrier, look-ahead
   constexpr int NST = 4 * ((BQ / 16) * (D / 16) / NW);  // dQ stores per wave per tile
+  auto tiles_in = [&](int lo, int hi) __attribute__((always_inline)) {  // |[lo, hi) ∩ [0, ntiles)|
+    return max(0, min(hi, ntiles) - max(lo, 0));
+  };
   const bool dq_first = PICO_BWD_STAGGER && D == 64 && wave >= NW / 2;  // D = 128: no registers to spare
-  Tc cur = {hq0, q00}, prev = cur;
-  int si_cur = 0, si_nxt = C::PD;  // ring slots of tiles t and t + PD
-  for (int t = 0; t < ntiles; ++t) {
-    stamp(t, 0);
-    // my pieces of tile t landed: issued in iteration j0 = t - PD, or in the prologue (j0 < 0)
-    const int j0 = t - C::PD;
-    if (j0 >= 0) {
-      int younger = j0 >= 1 ? NST : 0;
-      for (int j = j0 + 1; j < t; ++j) younger += (j + C::PD < ntiles ? my_np : 0) + (j >= 1 ? NST : 0);
-      wait_vmcnt(younger);
+  if constexpr (GT == 1) {  // one barrier per tile (D = 128: the variant below measured 3 % slower)
+    Tc cur = {hq0, q00}, prev = cur;
+    int si_cur = 0, si_nxt = PD;  // ring slots of tiles t and t + PD
+    for (int t = 0; t < ntiles; ++t) {
+      stamp(t, 0);
+      // my pieces of tile t landed: issued in iteration j0 = t - PD, or in the prologue (j0 < 0)
+      const int j0 = t - PD;
+      if (j0 >= 0) {
+        int younger = j0 >= 1 ? NST : 0;
+        for (int j = j0 + 1; j < t; ++j) younger += (j + PD < ntiles ? my_np : 0) + (j >= 1 ? NST : 0);
+        wait_vmcnt(younger);
+      }
+      // everyone's pieces of tile t visible, dS(t-1) visible, reads of slot (t-1) % NBUF and of
+      // dS image t % 2 (dQ of t-2) retired
+      lds_barrier();
+      stamp(t, 1);
+      if (t + PD < ntiles) issue(si_nxt, nxt);
+      if (dq_first && t >= 1) dq_tile((t - 1) & 1, prev);
+      stamp(t, 2);
+      if (active(cur.q0)) {
+        f32x16 s, dp;
+        bf16x8 sf[2];
+        sdp(si_cur, s, dp);
+        softmax_dkdv(si_cur, cur.q0, s, dp, sf);
+        stamp(t, 3);
+        ds_write(t & 1, sf);
+      }
+      stamp(t, 4);
+      if (!dq_first && t >= 1) dq_tile((t - 1) & 1, prev);
+      stamp(t, 5);
+      prev = cur;
+      advance(cur);
+      advance(nxt);
+      si_cur = next_slot(si_cur);
+      si_nxt = next_slot(si_nxt);
     }
-    // everyone's pieces of tile t visible, dS(t-1) visible, reads of slot (t-1) % NBUF and of
-    // dS image t % 2 (dQ of t-2) retired
     lds_barrier();
-    stamp(t, 1);
-    if (t + C::PD < ntiles) issue(si_nxt, nxt);
-    if (dq_first && t >= 1) dq_tile((t - 1) & 1, prev);
-    stamp(t, 2);
-    if (active(cur.q0)) {
-      f32x16 s, dp;
-      bf16x8 sf[2];
-      sdp(si_cur, s, dp);
-      softmax_dkdv(si_cur, cur.q0, s, dp, sf);
-      stamp(t, 3);
-      ds_write(t & 1, sf);
+    if (ntiles > 0) dq_tile((ntiles - 1) & 1, prev);
+  } else {
+    Tc cur = {hq0, q00}, dqc = cur;  // tile t's coordinates; the next dQ tile's (G tiles behind)
+    int si_cur = 0, si_nxt = PD;     // ring slots of tiles t and t + PD
+    int pc = 0, pq = 0;              // dS images of tile t and of the next dQ tile ((tile) % 2G)
+    auto next_img = [](int p) __attribute__((always_inline)) { return p + 1 == 2 * GT ? 0 : p + 1; };
+    auto dq_next = [&]() __attribute__((always_inline)) {
+      dq_tile(pq, dqc);
+      advance(dqc);
+      pq = next_img(pq);
+    };
+    int u = 0;
+    for (int t0 = 0; t0 < ntiles; t0 += GT, ++u) {
+      stamp(t0, 0);
+      // my pieces of this group's tiles landed: the last one, tile tl, went out in group gi (or the
+      // prologue); younger = the rest of gi's batch, gi's dQ stores, and every op of groups gi+1 .. u-1
+      const int tl = min(t0 + GT, ntiles) - 1;
+      if constexpr (PD == GT) {  // the group's pieces went out in group u - 1, before its G dQ tiles' stores
+        if (u >= 1) wait_vmcnt(u >= 2 ? GT * NST : 0);
+      } else if (tl - PD >= 0) {
+        const int gi = (tl - PD) / GT;
+        int younger = my_np * tiles_in(tl + 1, gi * GT + PD + GT) + (gi >= 1 ? GT * NST : 0);
+        for (int g = gi + 1; g < u; ++g) younger += my_np * tiles_in(g * GT + PD, g * GT + PD + GT) + (g >= 1 ? GT * NST : 0);
+        wait_vmcnt(younger);
+      }
+      // everyone's pieces of the group visible, the last group's dS images visible, reads of the slots
+      // about to be refilled and of the dS images about to be rewritten (dQ of group u - 2) retired
+      lds_barrier();
+      stamp(t0, 1);
+  #pragma unroll
+      for (int j = 0; j < GT; ++j) {
+        if (t0 + PD + j < ntiles) issue(si_nxt, nxt);
+        advance(nxt);
+        si_nxt = next_slot(si_nxt);
+      }
+  #pragma unroll PICO_BWD_GROUP_UNROLL
+      for (int j = 0; j < GT; ++j) {
+        if (dq_first && u >= 1) dq_next();
+        stamp(t0 + j, 2);
+        if (t0 + j < ntiles && active(cur.q0)) {
+          f32x16 s, dp;
+          bf16x8 sf[2];
+          sdp(si_cur, s, dp);
+          softmax_dkdv(si_cur, cur.q0, s, dp, sf);
+          stamp(t0 + j, 3);
+          ds_write(pc, sf);
+        }
+        stamp(t0 + j, 4);
+        if (!dq_first && u >= 1) dq_next();
+        stamp(t0 + j, 5);
+        advance(cur);
+        si_cur = next_slot(si_cur);
+        pc = next_img(pc);
+      }
     }
-    stamp(t, 4);
-    if (!dq_first && t >= 1) dq_tile((t - 1) & 1, prev);
-    stamp(t, 5);
-    prev = cur;
-    advance(cur);
-    advance(nxt);
-    si_cur = next_slot(si_cur);
-    si_nxt = next_slot(si_nxt);
+    lds_barrier();
+    for (int t = (u - 1) * GT; t < ntiles; ++t) dq_next();  // the last group's dQ tiles
   }
-  lds_barrier();
-  if (ntiles > 0) dq_tile((ntiles - 1) & 1, prev);
 
 #if PICO_BWD_STAMP
   if (D == 64 && blockIdx.x == 0) {
