@@ -97,6 +97,9 @@ def main():
     ap.add_argument("--grad-acc", type=int, default=32)
     ap.add_argument("--layers", type=int, default=LAYERS)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--backend", default="nccl",
+                    help="process-group backend: nccl (= RCCL over xGMI, the product) or gloo (tests: several "
+                         "ranks sharing one GPU, which RCCL refuses)")
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--cpu-seq", type=int, default=256)
     ap.add_argument("--fused-adam", type=int, default=1,
@@ -111,13 +114,17 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
-    torch.cuda.set_device(local_rank)
-    device = torch.device("cuda", local_rank)
+    # one GPU per rank; ranks beyond the visible GPUs share them round-robin (gloo rehearsal only)
+    device = torch.device("cuda", local_rank % torch.cuda.device_count())
+    torch.cuda.set_device(device)
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29561")
     os.environ.setdefault("RANK", str(rank))
     os.environ.setdefault("WORLD_SIZE", str(world))
-    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
+    if args.backend == "nccl":
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
+    else:
+        dist.init_process_group(args.backend, rank=rank, world_size=world)
 
     from picotron_amd import _lib as L
     from picotron_amd import process_group_manager as pgm
@@ -202,6 +209,8 @@ def main():
                 kernels[L.KERNEL_NAMES[k]] = {"total_ms": tot, "launches": n, "avg_us": 1e3 * tot / n}
         L.load().pico_prof_enable(0, 0)
 
+    allreduce = measure_allreduce(model, world, device) if world > 1 else None
+
     tokens = world * MBS * SEQ * args.grad_acc * args.steps
     value = tokens / elapsed
     tps_gpu = value / world
@@ -270,10 +279,43 @@ def main():
             "roofline": roofline,
             "kernels": kernels,
             "cpu_baseline": cpu_baseline,
+            "allreduce": allreduce,
         }
         os.write(json_fd, (json.dumps(out) + "\n").encode())
     dist.barrier()
     dist.destroy_process_group()
+
+
+XGMI_LINK_GBS, XGMI_LINKS = 153.0, 7  # MI355X xGMI: 7 point-to-point links per GPU, ~153 GB/s each
+
+
+def measure_allreduce(model, world, device, reps=3):
+    """Bus bandwidth of the DP gradient all-reduce (north_star: "all-reduce bus bandwidth against
+    xGMI peak"): the step's own fp32 bucket buffers (reference layout, ref bucket.py:84-129),
+    all-reduced back to back in readiness order (last bucket first, ref data_parallel.py:93-144),
+    timed after the throughput region with barrier + synchronize, max over ranks.
+    busbw = 2(W-1)/W * bytes / time (the ring algorithm's per-GPU wire bytes)."""
+    bufs = [b.grad_data for b in reversed(model.bucket_manager.buckets)]
+    nbytes = sum(b.numel() * b.element_size() for b in bufs)
+    for b in bufs:  # warm-up (communicator channels for every size class)
+        dist.all_reduce(b)
+    times = []
+    for _ in range(reps):
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for b in bufs:
+            dist.all_reduce(b)
+        torch.cuda.synchronize()
+        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        times.append(float(t.item()))
+    t = min(times)
+    busbw = 2.0 * (world - 1) / world * nbytes / t / 1e9
+    peak = XGMI_LINK_GBS * XGMI_LINKS
+    return {"buckets": len(bufs), "bytes": nbytes, "ms": round(1e3 * t, 3), "algbw_GBps": round(nbytes / t / 1e9, 1),
+            "busbw_GBps": round(busbw, 1), "peak_GBps": peak, "frac": round(busbw / peak, 4),
+            "single_link_GBps": XGMI_LINK_GBS, "timed_over": f"best of {reps} passes over all buckets, after the timed region"}
 
 
 def run_cpu_baseline(cfg, gpu_model, seq):

@@ -383,3 +383,28 @@ def test_graph_replay_with_dp_bucket(golden_loss):
     finally:
         pgm.process_group_manager = None
         dist.destroy_process_group()
+
+
+def test_bench_dp2_gloo_on_one_gpu():
+    """The N > 1 bench path end to end (DataParallelBucket + graph-replayed micro-batches + bucket
+    all-reduce + busbw measurement) with two ranks sharing this GPU. RCCL refuses two ranks on one
+    device, so the rehearsal uses the gloo backend; the 8-GPU RCCL run is the driver's."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="4")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(root, "bench.py"),
+           "--gpus", "2", "--backend", "gloo", "--layers", "2", "--grad-acc", "3", "--steps", "2", "--warmup", "1",
+           "--no-cpu-baseline"]
+    p = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2"
+    assert out["config"]["global_batch"] == 4 * 3 * 2
+    assert math.isfinite(out["loss_last"]) and out["loss_last"] < math.log(49152) + 0.1
+    ar = out["allreduce"]
+    assert ar["buckets"] > 0 and ar["bytes"] > 0 and ar["busbw_GBps"] > 0
