@@ -1,0 +1,102 @@
+"""Context-parallel ring attention across ranks on the GPU: RingAttentionFunc (ref
+picotron/context_parallel/context_parallel.py:17-110) with cp = 2 and 4 ranks sharing this one GPU,
+forward and backward on the gfx950 kernels, against whole-sequence attention on the same inputs.
+
+RCCL refuses two ranks on one device, so the ring's P2P runs over gloo with each transfer staged
+through host memory (a test-only ContextCommunicate; the product class is plain RCCL
+batch_isend_irecv). Every other piece — block kernels, LSE merge kernel, fp32 dQ accumulation, the
+dK/dV rotation order — is the product path.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+BF = torch.bfloat16
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _staged_comm_class(base):
+    import torch.distributed as dist
+
+    class HostStagedCommunicate(base):
+        """Same ring protocol as the product's ContextCommunicate; buffers cross over host memory."""
+
+        def send_recv(self, tensor_to_send, recv_tensor=None):
+            result = (torch.empty(tensor_to_send.shape, dtype=tensor_to_send.dtype, device=tensor_to_send.device)
+                      if recv_tensor is None else recv_tensor)
+            host_send = tensor_to_send.detach().contiguous().cpu()
+            host_recv = torch.empty(result.shape, dtype=result.dtype)
+            self._pending.append(dist.P2POp(dist.isend, host_send, self.send_rank, group=self.group))
+            self._pending.append(dist.P2POp(dist.irecv, host_recv, self.recv_rank, group=self.group))
+            self._landing = getattr(self, "_landing", []) + [(host_recv, result)]
+            return result
+
+        def wait(self):
+            super().wait()
+            for host, dev in self._landing:
+                dev.copy_(host)
+            self._landing = []
+
+    return HostStagedCommunicate
+
+
+def _worker(rank, world, port, causal):
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from picotron_amd import ops
+    from picotron_amd import process_group_manager as pgm
+    from picotron_amd.context_parallel import context_parallel as CP
+    pgm.setup_process_group_manager(tp_size=1, cp_size=world, pp_size=1, dp_size=1)
+    CP.ContextCommunicate = _staged_comm_class(CP.ContextCommunicate)
+
+    dev = "cuda:0"
+    B, S, Hq, D = 2, 1024, 4, 64
+    g = torch.Generator(device="cpu").manual_seed(21)  # identical full tensors on every rank
+    q, k, v, do = [torch.randn(B, S, Hq, D, generator=g).to(BF).to(dev) for _ in range(4)]
+    scale = D ** -0.5
+    # whole-sequence reference through the same kernels (pinned to the fp64 oracle by test_kernels_gpu)
+    qf, kf, vf = [t.clone().requires_grad_(True) for t in (q, k, v)]
+    of = ops.flash_attn_func(qf, kf, vf, softmax_scale=scale, causal=causal)
+    of.backward(do)
+    n = S // world
+    sl = slice(rank * n, (rank + 1) * n)
+    ql, kl, vl = [t[:, sl].contiguous().requires_grad_(True) for t in (q, k, v)]
+    ol = CP.ring_attention(ql, kl, vl, scale, causal)
+    ol.backward(do[:, sl].contiguous())
+    torch.cuda.synchronize()
+
+    def rel(a, b):
+        a, b = a.double(), b.double()
+        return float((a - b).norm() / b.norm())
+
+    errs = {"out": rel(ol, of[:, sl]), "dq": rel(ql.grad, qf.grad[:, sl]), "dk": rel(kl.grad, kf.grad[:, sl]),
+            "dv": rel(vl.grad, vf.grad[:, sl])}
+    # bf16 outputs of two differently-blocked fp32 computations: within a few bf16 roundings
+    tol = {"out": 4e-3, "dq": 8e-3, "dk": 8e-3, "dv": 8e-3}
+    bad = {kk: e for kk, e in errs.items() if not e < tol[kk]}
+    dist.barrier()
+    dist.destroy_process_group()
+    if bad:
+        raise AssertionError(f"rank {rank} cp={world} causal={causal}: {bad} (all: {errs})")
+
+
+@pytest.mark.parametrize("world,causal", [(2, True), (4, True), (2, False)])
+def test_ring_attention_multi_rank(world, causal):
+    mp.start_processes(_worker, args=(world, _free_port(), causal), nprocs=world, join=True, start_method="spawn")
