@@ -14,6 +14,12 @@
 // fp32 math throughout (torch: fp32 opmath inside log_softmax, bf16 log-probs in between).
 #include "common.h"
 
+// PICO_CE_THREADS: threads per logits row in the fused forward+gradient kernel (A/B build variants)
+#ifndef PICO_CE_THREADS
+#define PICO_CE_THREADS 512
+#endif
+constexpr float LOG2E = 1.4426950408889634f;
+
 namespace {
 
 PICO_DEV float wave_max_dpp(float v) {
@@ -27,6 +33,7 @@ PICO_DEV float wave_max_dpp(float v) {
   return fmaxf(__uint_as_float(r32[0]), __uint_as_float(r32[1]));
 }
 
+template <int NT>
 PICO_DEV float block_reduce(float v, float* red, bool is_max) {
   v = is_max ? wave_max_dpp(v) : wave_sum_dpp(v);  // DPP / permlane, no LDS round trips
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -35,7 +42,7 @@ PICO_DEV float block_reduce(float v, float* red, bool is_max) {
   __syncthreads();
   float r = red[0];
 #pragma unroll
-  for (int k = 1; k < 4; ++k) r = is_max ? fmaxf(r, red[k]) : r + red[k];
+  for (int k = 1; k < NT / 64; ++k) r = is_max ? fmaxf(r, red[k]) : r + red[k];
   return r;
 }
 
@@ -58,7 +65,7 @@ __global__ __launch_bounds__(256) void ce_fwd_kernel(const bf16_t* __restrict__ 
       for (int j = 0; j < 8; ++j) m = fmaxf(m, bf2f(v[c][j]));
     }
   }
-  m = block_reduce(m, red, true);
+  m = block_reduce<256>(m, red, true);
   float s = 0.f;
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
@@ -68,7 +75,7 @@ __global__ __launch_bounds__(256) void ce_fwd_kernel(const bf16_t* __restrict__ 
       for (int j = 0; j < 8; ++j) s += __builtin_amdgcn_exp2f((bf2f(v[c][j]) - m) * 1.4426950408889634f);
     }
   }
-  s = block_reduce(s, red, false);
+  s = block_reduce<256>(s, red, false);
   if (threadIdx.x == 0) {
     const float l = m + __logf(s);
     const int64_t t = target[row];
@@ -111,12 +118,12 @@ __global__ __launch_bounds__(256) void ce_bwd_kernel(const bf16_t* __restrict__ 
 // registers) is overwritten with dlogits = (softmax - onehot(t)) * (*gscale) (0 for ignored rows). One
 // read + one write of the logits instead of fwd read + bwd read + bwd write; the caller applies the
 // upstream gradient later (it scales the LM-head GEMMs' results, not the logits).
-template <int NCH>
-__global__ __launch_bounds__(256) void ce_fwd_grad_kernel(bf16_t* __restrict__ logits, int64_t ld,
+template <int NCH, int NT>
+__global__ __launch_bounds__(NT) void ce_fwd_grad_kernel(bf16_t* __restrict__ logits, int64_t ld,
                                                           const int64_t* __restrict__ target, float* __restrict__ lse,
                                                           float* __restrict__ loss, const float* __restrict__ gscale,
                                                           int vocab, int64_t ignore) {
-  __shared__ float red[4];
+  __shared__ float red[NT / 64];
   const int64_t row = blockIdx.x;
   bf16_t* x = logits + row * ld;
   const int nchunk = vocab / 8;
@@ -127,49 +134,54 @@ __global__ __launch_bounds__(256) void ce_fwd_grad_kernel(bf16_t* __restrict__ l
   float m = -INFINITY;
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
-    const int ch = threadIdx.x + 256 * c;
+    const int ch = threadIdx.x + NT * c;
     if (ch < nchunk) {
       v[c] = *reinterpret_cast<const u16x8*>(x + 8 * ch);
 #pragma unroll
       for (int j = 0; j < 8; ++j) m = fmaxf(m, bf2f(v[c][j]));
     }
   }
-  m = block_reduce(m, red, true);
+  m = block_reduce<NT>(m, red, true);
   float s = 0.f;
+  const float nm2 = -m * LOG2E;  // exp(x - m) = exp2(fma(x, log2 e, -m log2 e)): one FMA per logit
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
-    const int ch = threadIdx.x + 256 * c;
+    const int ch = threadIdx.x + NT * c;
     if (ch < nchunk) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) s += __builtin_amdgcn_exp2f((bf2f(v[c][j]) - m) * 1.4426950408889634f);
+      for (int j = 0; j < 8; ++j) s += __builtin_amdgcn_exp2f(__builtin_fmaf(bf2f(v[c][j]), LOG2E, nm2));
     }
   }
-  s = block_reduce(s, red, false);
+  s = block_reduce<NT>(s, red, false);
   const float l = m + __logf(s);
   if (threadIdx.x == 0) {
     lse[row] = l;
     loss[row] = skip ? 0.f : l - xt;
   }
   const float g = skip ? 0.f : *gscale;
+  // softmax * g = exp2(x log2 e - l log2 e + log2 g): one FMA + one exp2 per logit (g = 0 -> log2 g =
+  // -inf -> 0 for ignored rows); the one-hot term is applied afterwards by the lane that owns the
+  // target (its later store to the same address wins)
+  const float c2 = __builtin_fmaf(-l, LOG2E, __log2f(g));
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
-    const int ch = threadIdx.x + 256 * c;
+    const int ch = threadIdx.x + NT * c;
     if (ch < nchunk) {
       u16x8 o;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float p = __builtin_amdgcn_exp2f((bf2f(v[c][j]) - l) * 1.4426950408889634f);
-        if (8 * ch + j == t) p -= 1.f;
-        o[j] = f2bf(p * g);
-      }
+      for (int j = 0; j < 8; ++j) o[j] = f2bf(__builtin_amdgcn_exp2f(__builtin_fmaf(bf2f(v[c][j]), LOG2E, c2)));
       *reinterpret_cast<u16x8*>(x + 8 * ch) = o;
     }
   }
+  if (!skip && (int)(t >> 3) % NT == (int)threadIdx.x) {
+    const float pt = __builtin_amdgcn_exp2f(__builtin_fmaf(xt, LOG2E, c2));
+    x[t] = f2bf(pt - g);
+  }
 }
 
-int nch_for(int64_t vocab) {
-  const int64_t per = (vocab / 8 + 255) / 256;
-  for (int n : {4, 8, 16, 24, 32, 48, 64})
+int nch_for(int64_t vocab, int nt = 256) {
+  const int64_t per = (vocab / 8 + nt - 1) / nt;
+  for (int n : {2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64})
     if (per <= n) return n;
   return -1;
 }
@@ -178,6 +190,10 @@ int nch_for(int64_t vocab) {
 
 #define CE_SWITCH(NCHV, CALL)                      \
   switch (NCHV) {                                  \
+    case 2: { constexpr int N = 2; CALL; } break;   \
+    case 3: { constexpr int N = 3; CALL; } break;   \
+    case 6: { constexpr int N = 6; CALL; } break;   \
+    case 12: { constexpr int N = 12; CALL; } break; \
     case 4: { constexpr int N = 4; CALL; } break;   \
     case 8: { constexpr int N = 8; CALL; } break;   \
     case 16: { constexpr int N = 16; CALL; } break; \
@@ -208,14 +224,14 @@ extern "C" int pico_cross_entropy_fwd_grad(void* logits, int64_t ld, const int64
                                            void* stream) {
   PICO_REQUIRE(rows >= 0 && vocab > 0 && vocab % 8 == 0 && ld % 8 == 0 && ld >= vocab,
                "pico_cross_entropy_fwd_grad: vocab (%lld) and row stride must be multiples of 8", (long long)vocab);
-  const int nch = nch_for(vocab);
+  const int nch = nch_for(vocab, PICO_CE_THREADS);
   PICO_REQUIRE(nch > 0, "pico_cross_entropy_fwd_grad: vocab %lld too large", (long long)vocab);
   PICO_REQUIRE(rows < (1ll << 31), "pico_cross_entropy_fwd_grad: too many rows");
   if (rows == 0) return 0;
   PICO_REQUIRE(logits && target && lse && loss && grad_scale, "pico_cross_entropy_fwd_grad: null pointer");
   hipStream_t s = (hipStream_t)stream;
   CE_SWITCH(nch, PICO_LAUNCH(PICO_K_CE_FWD, "cross_entropy_fwd_grad", s,
-                             ce_fwd_grad_kernel<N><<<(int)rows, 256, 0, s>>>((bf16_t*)logits, ld, target, lse, loss,
+                             ce_fwd_grad_kernel<N, PICO_CE_THREADS><<<(int)rows, PICO_CE_THREADS, 0, s>>>((bf16_t*)logits, ld, target, lse, loss,
                                                                              grad_scale, (int)vocab, ignore_index)))
   return 0;
 }

@@ -36,6 +36,16 @@ def main(iters=50):
     xt = torch.empty(H, T, dtype=bf, device=dev)
     wgu = torch.randn(2 * I, H, dtype=bf, device=dev)
     wgut = torch.empty(H, 2 * I, dtype=bf, device=dev)
+    logits = torch.randn(T, V, dtype=bf, device=dev) * 4
+    tgt = torch.randint(0, V, (T,), device=dev)
+    lse = torch.empty(T, dtype=torch.float32, device=dev)
+    loss_rows = torch.empty(T, dtype=torch.float32, device=dev)
+    gscale = torch.full((1,), 1.0 / T, dtype=torch.float32, device=dev)
+
+    def run_ce():  # fused LM-head CE pass: dlogits written over the logits (values drift; timing only)
+        L.check(L.load().pico_cross_entropy_fwd_grad(L.ptr(logits), logits.stride(0), L.ptr(tgt), L.ptr(lse),
+                                                     L.ptr(loss_rows), L.ptr(gscale), T, V, -100, L.stream_of(logits)),
+                "pico_cross_entropy_fwd_grad")
 
     def run_norm():
         y, res = ops.rms_norm(x, w, 1e-5, residual=r, prenorm=True)
@@ -52,12 +62,13 @@ def main(iters=50):
                             ops._swiglu_bwd(dh, gu, gu[:, I:], dgu, dgu[:, I:], T, I, 2 * I, I)),
          [L.K_SWIGLU_FWD, L.K_SWIGLU_BWD]),
         ("embedding", lambda: ops._embedding_bwd_into(gemb, ids, dy_emb, 1.0), [L.K_EMBEDDING_BWD]),
+        ("ce_fwd_grad", run_ce, [L.K_CE_FWD]),
         ("transpose_x", lambda: ops.transpose_2d(x.detach(), out=xt), [L.K_TRANSPOSE]),
         ("transpose_wgu", lambda: ops.transpose_2d(wgu, out=wgut), [L.K_TRANSPOSE]),
     ]
     work = {L.K_RMSNORM_FWD: 4 * T * H * 2 + 4 * T, L.K_RMSNORM_BWD: 4 * T * H * 2 + 4 * T,
             L.K_ROPE: 2 * T * 2 * NH * D * 2, L.K_SWIGLU_FWD: 3 * T * I * 2, L.K_SWIGLU_BWD: 5 * T * I * 2,
-            L.K_EMBEDDING_BWD: T * H * 2 + 2 * T * H * 2}
+            L.K_EMBEDDING_BWD: T * H * 2 + 2 * T * H * 2, L.K_CE_FWD: 2 * T * V * 2}
     tbytes = {"transpose_x": 2 * T * H * 2, "transpose_wgu": 2 * 2 * I * H * 2}
     for name, fn, kids in cases:
         if L.K_TRANSPOSE in kids:
