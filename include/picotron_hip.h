@@ -23,6 +23,7 @@
  *   pico_scale_f32            <- grad_data /= process_group_size     (ref picotron/data_parallel/bucket.py:30)
  *   pico_cross_entropy_fwd/_bwd <- F.cross_entropy(logits, target, reduction='mean')
  *                                 (ref train.py:46-49, picotron/pipeline_parallel/pipeline_parallel.py:68,98)
+ *   pico_sort_ids             <- the stable id sort inside F.embedding's backward (ref picotron/model.py:223-224)
  *   pico_embedding_bwd        <- backward of F.embedding (ref picotron/model.py:223-224) + the micro-batch
  *                                 gradient accumulation (data_parallel.py:131 / autograd's grad += dW)
  *   pico_transpose_bf16       <- no reference call: lays out x^T / W^T for the faster hipBLASLt forms of
@@ -67,7 +68,8 @@ enum {
   PICO_K_CE_BWD = 17,
   PICO_K_TRANSPOSE = 18,
   PICO_K_ATTN_BWD_DKV = 19,
-  PICO_K_COUNT = 20
+  PICO_K_SORT_IDS = 20,
+  PICO_K_COUNT = 21
 };
 
 int pico_abi_version(void);
@@ -195,6 +197,12 @@ int pico_cast_f32_bf16(const float* src, void* dst, int64_t n, void* stream);
  * for every id present: grad[id] = (grad[id] + sum of its dy rows in position order) * scale. */
 int pico_embedding_bwd(const int64_t* sorted_ids, const int64_t* sorted_pos, const void* dy, void* grad,
                        int64_t n_tokens, int64_t dim, int grad_is_f32, float scale, void* stream);
+/* Stable ascending sort of n <= 8192 token ids in [0, vocab), vocab <= 2^19 (int64, device) with their
+ * positions: the input pico_embedding_bwd wants, bit-identical to torch.sort(ids, stable=True)
+ * (which the reference's F.embedding backward does inside ATen). One workgroup, LDS bitonic sort of
+ * (id << 13 | position) keys. */
+int pico_sort_ids(const int64_t* ids, int64_t n, int64_t vocab, int64_t* sorted_ids, int64_t* sorted_pos,
+                  void* stream);
 
 /* ---- softmax cross-entropy (mean over non-ignored rows) ----
  * logits: [rows, vocab] bf16, row stride ld (elements); target: [rows] int64.

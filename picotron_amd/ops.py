@@ -409,9 +409,22 @@ def dgrad(dy2, W, params):
     return torch.matmul(dy2, W)
 
 
+def sort_ids(flat, vocab):
+    """torch.sort(flat, stable=True) of int64 token ids on pico_sort_ids (one LDS workgroup) when it fits
+    (<= 8192 ids, vocab <= 2^19); the same result, bit for bit."""
+    if flat.numel() > 8192 or vocab > (1 << 19) or flat.dtype != torch.int64:
+        return torch.sort(flat, stable=True)
+    flat = flat.contiguous()
+    sids = torch.empty_like(flat)
+    spos = torch.empty_like(flat)
+    _lib.check(_lib.load().pico_sort_ids(_lib.ptr(flat), flat.numel(), int(vocab), _lib.ptr(sids), _lib.ptr(spos),
+                                         _lib.stream_of(flat)), "pico_sort_ids")
+    return sids, spos
+
+
 def _embedding_bwd_into(grad, ids, dy, scale):
     flat = ids.reshape(-1)
-    sids, spos = torch.sort(flat, stable=True)
+    sids, spos = sort_ids(flat, grad.shape[0])
     dy2 = dy.reshape(-1, dy.shape[-1])
     if not dy2.is_contiguous():
         dy2 = dy2.contiguous()

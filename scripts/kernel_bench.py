@@ -61,7 +61,7 @@ def main(iters=50):
         ("swiglu", lambda: (ops._swiglu_fwd(gu, gu[:, I:], h, T, I, 2 * I, I),
                             ops._swiglu_bwd(dh, gu, gu[:, I:], dgu, dgu[:, I:], T, I, 2 * I, I)),
          [L.K_SWIGLU_FWD, L.K_SWIGLU_BWD]),
-        ("embedding", lambda: ops._embedding_bwd_into(gemb, ids, dy_emb, 1.0), [L.K_EMBEDDING_BWD]),
+        ("embedding", lambda: ops._embedding_bwd_into(gemb, ids, dy_emb, 1.0), [L.K_SORT_IDS, L.K_EMBEDDING_BWD]),
         ("ce_fwd_grad", run_ce, [L.K_CE_FWD]),
         ("transpose_x", lambda: ops.transpose_2d(x.detach(), out=xt), [L.K_TRANSPOSE]),
         ("transpose_wgu", lambda: ops.transpose_2d(wgu, out=wgut), [L.K_TRANSPOSE]),

@@ -382,6 +382,22 @@ def test_grad_accum_and_cast_bit_exact():
     assert torch.equal(v, ref)
 
 
+@pytest.mark.parametrize("n,vocab", [(1, 10), (7, 3), (1000, 49152), (4096, 49152), (4096, 17), (8192, 1 << 19),
+                                     (3000, 32000)])
+def test_sort_ids_matches_torch_stable_sort(n, vocab):
+    """pico_sort_ids == torch.sort(ids, stable=True): ids and positions bit for bit (heavy duplicates,
+    non-power-of-two counts, the largest id / count the packed key allows)."""
+    ops = _ops()
+    g = torch.Generator(device="cpu").manual_seed(n + vocab)
+    ids = torch.randint(0, vocab, (n,), generator=g).to(DEV)
+    if n > 2:
+        ids[-1] = vocab - 1
+        ids[0] = vocab - 1
+    s1, p1 = ops.sort_ids(ids, vocab)
+    s2, p2 = torch.sort(ids, stable=True)
+    assert torch.equal(s1, s2) and torch.equal(p1, p2)
+
+
 # ------------------------------------------------------------------------------------------ embedding
 @pytest.mark.parametrize("grad_dtype", [torch.bfloat16, torch.float32])
 def test_embedding_bwd_matches_dense(grad_dtype):
