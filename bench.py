@@ -105,6 +105,9 @@ def main():
     ap.add_argument("--fused-adam", type=int, default=1,
                     help="AdamW(fused=True): the reference's use_fused_adam config (ref template/base_config.json:18, "
                          "train.py:204-207)")
+    ap.add_argument("--optimizer", default="pico", choices=["pico", "torch"],
+                    help="pico: picotron_amd.optim.AdamW (pico_adamw_bf16, one launch); torch: "
+                         "torch.optim.AdamW (fused per --fused-adam), the reference's optimizer")
     ap.add_argument("--graphs", type=int, default=1,
                     help="replay non-syncing micro-batches as a HIP graph (1) or run them eagerly (0)")
     args = ap.parse_args()
@@ -143,7 +146,11 @@ def main():
     if world > 1:
         model = DataParallelBucket(model)
     # ref train.py:204-209: AdamW(lr), fused when the config's use_fused_adam is set (template default true)
-    opt = torch.optim.AdamW(model.parameters(), lr=3e-4, **({"fused": True} if args.fused_adam else {}))
+    if args.optimizer == "pico":
+        from picotron_amd.optim import AdamW
+        opt = AdamW(model.parameters(), lr=3e-4)
+    else:
+        opt = torch.optim.AdamW(model.parameters(), lr=3e-4, **({"fused": True} if args.fused_adam else {}))
     loader = SyntheticDataLoader(MBS, SEQ, args.grad_acc, cfg.vocab_size, seed=1234, kind="uniform",
                                  num_batches=args.grad_acc, device=device)
     log(f"[rank {rank}] model {num_params / 1e9:.3f}B params built in {time.time() - t0:.1f}s")
@@ -268,7 +275,9 @@ def main():
             "dtype": "bf16",
             "data": "synthetic (uniform token ids, reference random init)",
             "config": {"workload": "SmolLM-1.7B 15 layers, seq 1024, micro-batch 4, grad_acc %d per GPU, "
-                                   "full training step (fwd+bwd+AdamW%s)" % (args.grad_acc, " fused" if args.fused_adam else ""),
+                                   "full training step (fwd+bwd+AdamW%s)" % (
+                                       args.grad_acc, " pico_adamw_bf16" if args.optimizer == "pico" else
+                                       (" torch fused" if args.fused_adam else " torch")),
                        "model": "SmolLM-1.7B-%dL" % args.layers, "global_batch": MBS * args.grad_acc * world,
                        "seq_len": SEQ, "micro_batch": MBS, "grad_acc": args.grad_acc, "parallelism": f"dp{world}"},
             "tokens_per_sec_per_gpu": round(tps_gpu, 1),

@@ -23,6 +23,7 @@
  *   pico_scale_f32            <- grad_data /= process_group_size     (ref picotron/data_parallel/bucket.py:30)
  *   pico_cross_entropy_fwd/_bwd <- F.cross_entropy(logits, target, reduction='mean')
  *                                 (ref train.py:46-49, picotron/pipeline_parallel/pipeline_parallel.py:68,98)
+ *   pico_adamw_bf16           <- torch.optim.AdamW(..., fused=True).step() (ref train.py:204-209,235)
  *   pico_sort_ids             <- the stable id sort inside F.embedding's backward (ref picotron/model.py:223-224)
  *   pico_embedding_bwd        <- backward of F.embedding (ref picotron/model.py:223-224) + the micro-batch
  *                                 gradient accumulation (data_parallel.py:131 / autograd's grad += dW)
@@ -69,7 +70,8 @@ enum {
   PICO_K_TRANSPOSE = 18,
   PICO_K_ATTN_BWD_DKV = 19,
   PICO_K_SORT_IDS = 20,
-  PICO_K_COUNT = 21
+  PICO_K_ADAMW = 21,
+  PICO_K_COUNT = 22
 };
 
 int pico_abi_version(void);
@@ -203,6 +205,18 @@ int pico_embedding_bwd(const int64_t* sorted_ids, const int64_t* sorted_pos, con
  * (id << 13 | position) keys. */
 int pico_sort_ids(const int64_t* ids, int64_t n, int64_t vocab, int64_t* sorted_ids, int64_t* sorted_pos,
                   void* stream);
+
+/* ---- AdamW step over a whole parameter list (one launch) ----
+ * Replaces torch.optim.AdamW(params, lr, fused=True).step() (ref train.py:13,204-209,235) for bf16
+ * parameters with bf16 exp_avg / exp_avg_sq (torch keeps the states in the parameter dtype).
+ * tensors: device int64 [n_tensors][4] = (param, grad, exp_avg, exp_avg_sq) addresses; sizes: device
+ * int64 [n_tensors] numel; chunks: device int64 [n_chunks][2] = (tensor index, first element), one
+ * per pico_adamw_chunk_elems() elements of each tensor. step: the step number after increment (>= 1).
+ * Same expression order and types as ATen's fused AdamW (decoupled weight decay). */
+int64_t pico_adamw_chunk_elems(void);
+int pico_adamw_bf16(const int64_t* tensors, const int64_t* sizes, const int64_t* chunks, int64_t n_chunks,
+                    double lr, double beta1, double beta2, double eps, double weight_decay, int64_t step,
+                    void* stream);
 
 /* ---- softmax cross-entropy (mean over non-ignored rows) ----
  * logits: [rows, vocab] bf16, row stride ld (elements); target: [rows] int64.

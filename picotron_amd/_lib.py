@@ -16,14 +16,14 @@ LIB_PATH = os.environ.get("PICO_LIB_PATH") or os.path.join(os.path.dirname(os.pa
 K_RMSNORM_FWD, K_RMSNORM_BWD, K_RMSNORM_DW, K_ROPE = 1, 2, 3, 4
 K_SWIGLU_FWD, K_SWIGLU_BWD, K_ATTN_FWD, K_ATTN_BWD_PRE = 5, 6, 7, 8
 K_ATTN_BWD, K_ATTN_BWD_DQ, K_GRAD_ACCUM, K_CAST, K_SCALE, K_ATTN_MERGE = 9, 10, 11, 12, 13, 14
-K_EMBEDDING_BWD, K_CE_FWD, K_CE_BWD, K_TRANSPOSE, K_ATTN_BWD_DKV, K_SORT_IDS = 15, 16, 17, 18, 19, 20
+K_EMBEDDING_BWD, K_CE_FWD, K_CE_BWD, K_TRANSPOSE, K_ATTN_BWD_DKV, K_SORT_IDS, K_ADAMW = 15, 16, 17, 18, 19, 20, 21
 KERNEL_NAMES = {
     K_RMSNORM_FWD: "rmsnorm_fwd", K_RMSNORM_BWD: "rmsnorm_bwd", K_RMSNORM_DW: "rmsnorm_dw", K_ROPE: "rope",
     K_SWIGLU_FWD: "swiglu_fwd", K_SWIGLU_BWD: "swiglu_bwd", K_ATTN_FWD: "attn_fwd",
     K_ATTN_BWD_PRE: "attn_bwd_pre", K_ATTN_BWD: "attn_bwd", K_ATTN_BWD_DQ: "attn_bwd_dq",
     K_GRAD_ACCUM: "grad_accum", K_CAST: "cast_f32_bf16", K_SCALE: "scale_f32", K_ATTN_MERGE: "attn_merge",
     K_EMBEDDING_BWD: "embedding_bwd", K_CE_FWD: "cross_entropy_fwd", K_CE_BWD: "cross_entropy_bwd",
-    K_TRANSPOSE: "transpose_bf16", K_ATTN_BWD_DKV: "attn_bwd_dkv", K_SORT_IDS: "sort_ids",
+    K_TRANSPOSE: "transpose_bf16", K_ATTN_BWD_DKV: "attn_bwd_dkv", K_SORT_IDS: "sort_ids", K_ADAMW: "adamw",
 }
 
 ATTN_DQ_F32_ACCUM = 1
@@ -76,6 +76,9 @@ _SIGNATURES = {
     "pico_cast_f32_bf16": (ctypes.c_int, [c_vp, c_vp, c_i64, c_vp]),
     "pico_embedding_bwd": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, ctypes.c_int, ctypes.c_float, c_vp]),
     "pico_sort_ids": (ctypes.c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, c_vp]),
+    "pico_adamw_chunk_elems": (c_i64, []),
+    "pico_adamw_bf16": (ctypes.c_int, [c_vp, c_vp, c_vp, c_i64, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                       ctypes.c_double, ctypes.c_double, c_i64, c_vp]),
     "pico_cross_entropy_fwd": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp]),
     "pico_cross_entropy_fwd_grad": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp]),
     "pico_cross_entropy_bwd": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp]),
