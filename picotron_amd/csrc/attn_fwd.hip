@@ -40,6 +40,16 @@
 #define PICO_FWD_EARLY_V -1
 #endif
 
+//   PICO_FWD_NBUF_D64 / PICO_FWD_WPE_D64: ring slots and waves per SIMD for D = 64. 2 / 4 (shipped):
+//     four 32-KiB workgroups per CU, prefetch distance 1, 128 VGPRs without spills; 3 / 3: three
+//     48-KiB workgroups per CU. Measured C2 causal 36.0 -> 34.8 us, full 54.9 -> 52.5, GQA 33.5 -> 32.3.
+#ifndef PICO_FWD_NBUF_D64
+#define PICO_FWD_NBUF_D64 2
+#endif
+#ifndef PICO_FWD_WPE_D64
+#define PICO_FWD_WPE_D64 4
+#endif
+
 namespace {
 
 constexpr int BM = 128;  // query rows per workgroup (32 per wave)
@@ -65,10 +75,10 @@ struct FwdCfg {
   static constexpr int KIMG = BN * 32;                  // bytes per 16-wide K image
   static constexpr int VIMG = BN * 64;                  // bytes per 32-wide V image
   static constexpr int SLOT = 2 * BN * D * 2;           // K + V of one tile
-  static constexpr int NBUF = D == 64 ? 3 : 2;          // LDS: 48 KiB (D=64) / 64 KiB (D=128) per WG
+  static constexpr int NBUF = D == 64 ? PICO_FWD_NBUF_D64 : 2;  // LDS: 16 KiB (D=64) / 32 KiB (D=128) per slot
   static constexpr int NI = 2 * KS + 4 * DT;            // 1-KiB DMA pieces per tile
   static constexpr int NIW = NI / 4;                    // ... per wave
-  static constexpr int WAVES_PER_EU = D == 64 ? 3 : 2;
+  static constexpr int WAVES_PER_EU = D == 64 ? PICO_FWD_WPE_D64 : 2;
 };
 
 // max over both lane halves (lane r and r + 32 hold the same query row)
