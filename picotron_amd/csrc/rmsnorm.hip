@@ -261,26 +261,31 @@ int launch_rmsnorm_bwd(const void* dy, const void* dres, const void* x, const vo
 }
 
 // dw[col] = sum over the workgroup partials, in a fixed order (deterministic): a 256-thread
-// workgroup covers 32 columns x 8 row-slices; each thread sums its slice (loads coalesced across the
-// 32 columns), then the 8 slices are combined through LDS in slice order.
+// workgroup covers DW_COLS columns x (256 / DW_COLS) row-slices; each thread sums its slice (loads
+// coalesced across the columns), then the slices are combined through LDS in slice order.
 // MODE 0: dw (bf16) = sum; 1: dw (bf16) = bf16(dw + sum); 2: dw (fp32) = (dw + sum) * scale
+#ifndef PICO_RMS_DW_COLS
+#define PICO_RMS_DW_COLS 32
+#endif
+constexpr int DW_COLS = PICO_RMS_DW_COLS, DW_SL = 256 / DW_COLS;
+
 template <int MODE>
 __global__ __launch_bounds__(256) void rmsnorm_dw_kernel(const float* __restrict__ part, void* __restrict__ dw, int nblk,
                                                          int cols, float scale) {
-  __shared__ float red[8][32];
-  const int c = threadIdx.x & 31, sl = threadIdx.x >> 5;
-  const int col = blockIdx.x * 32 + c;
+  __shared__ float red[DW_SL][DW_COLS];
+  const int c = threadIdx.x % DW_COLS, sl = threadIdx.x / DW_COLS;
+  const int col = blockIdx.x * DW_COLS + c;
   float s = 0.f;
   if (col < cols) {
 #pragma unroll 8
-    for (int b = sl; b < nblk; b += 8) s += part[(int64_t)b * cols + col];
+    for (int b = sl; b < nblk; b += DW_SL) s += part[(int64_t)b * cols + col];
   }
   red[sl][c] = s;
   __syncthreads();
   if (sl == 0 && col < cols) {
     float t = red[0][c];
 #pragma unroll
-    for (int k = 1; k < 8; ++k) t += red[k][c];
+    for (int k = 1; k < DW_SL; ++k) t += red[k][c];
     if constexpr (MODE == 0) {
       ((bf16_t*)dw)[col] = f2bf(t);
     } else if constexpr (MODE == 1) {
@@ -305,10 +310,14 @@ int maxc_for(int64_t cols) {
 
 constexpr int bwd_waves(int maxc) { return maxc <= 2 ? 16 : (maxc == 4 ? 8 : 4); }
 
+#ifndef PICO_RMS_BWD_MAXB
+#define PICO_RMS_BWD_MAXB 256
+#endif
+
 int bwd_blocks(int64_t rows, int64_t cols) {  // one workgroup per CU at most: few dw partial rows
   const int nw = bwd_waves(maxc_for(cols));
   int64_t nb = (rows + nw - 1) / nw;
-  return (int)(nb < 256 ? nb : 256);
+  return (int)(nb < PICO_RMS_BWD_MAXB ? nb : PICO_RMS_BWD_MAXB);
 }
 
 }  // namespace
@@ -408,7 +417,7 @@ int pico_rmsnorm_bwd_acc(const void* dy, const void* dresidual, const void* x, c
   }
   if (rc) return rc;
 
-  const int g = pico_cdiv(cols, 32);
+  const int g = pico_cdiv(cols, DW_COLS);
   if (dw_mode == 0) {
     PICO_LAUNCH(PICO_K_RMSNORM_DW, "rmsnorm_dw", s, rmsnorm_dw_kernel<0><<<g, 256, 0, s>>>(part, dweight, nb, c, 1.f));
   } else if (dw_mode == 1) {
