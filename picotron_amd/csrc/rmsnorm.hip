@@ -76,12 +76,17 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd_kernel(const bf16_t* __restri
 
 // Forward that also writes y^T ([cols, rows], row stride ldt): the x^T the following projection's
 // weight-gradient GEMM reads (TT form), at the cost of one extra write instead of a transpose pass.
-// One 512-thread workgroup per 32 rows (wave w: rows w, w + 8, ...; a lane owns 8 contiguous columns
+// One 1024-thread workgroup per 32 rows (wave w: rows w, w + 16; a lane owns 8 contiguous columns
 // per 512-column chunk as in rmsnorm_fwd_kernel); y is also staged into an LDS tile [32][cols + 8]
 // (128.5 KiB at cols = 2048), then each thread stores 8-token segments of y^T rows (4 x 16 B per
 // 64-B row segment). Requires cols == MAXC * 512 and rows % 32 == 0 (host checks).
+#ifndef PICO_RMS_FWDT_WAVES
+#define PICO_RMS_FWDT_WAVES 16
+#endif
+constexpr int FWDT_WAVES = PICO_RMS_FWDT_WAVES;  // waves per 32-row tile (rows per wave = 32 / FWDT_WAVES)
+
 template <int MAXC, bool RES>
-__global__ __launch_bounds__(512) void rmsnorm_fwd_t_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
+__global__ __launch_bounds__(FWDT_WAVES * 64) void rmsnorm_fwd_t_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
                                                             const bf16_t* __restrict__ w, bf16_t* __restrict__ y,
                                                             bf16_t* __restrict__ res_out, float* __restrict__ rstd,
                                                             bf16_t* __restrict__ yt, int64_t ldt, float eps) {
@@ -89,11 +94,11 @@ __global__ __launch_bounds__(512) void rmsnorm_fwd_t_kernel(const bf16_t* __rest
   extern __shared__ __attribute__((aligned(16))) unsigned short tile[];  // [32][PITCH]
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int64_t r0 = (int64_t)blockIdx.x * 32;
-  constexpr int RPW = 4;  // rows per wave (rows wid + 8 k): every load of the four rows issued first
+  constexpr int RPW = 32 / FWDT_WAVES;  // rows per wave (rows wid + FWDT_WAVES k): every load issued first
   u16x8 xr[RPW][MAXC], rr[RPW][MAXC];
 #pragma unroll
   for (int k = 0; k < RPW; ++k) {
-    const int64_t row = r0 + wid + 8 * k;
+    const int64_t row = r0 + wid + FWDT_WAVES * k;
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) {
       const int col = (c * 64 + lane) * 8;
@@ -104,7 +109,7 @@ __global__ __launch_bounds__(512) void rmsnorm_fwd_t_kernel(const bf16_t* __rest
   float ss[RPW];
 #pragma unroll
   for (int k = 0; k < RPW; ++k) {
-    const int64_t row = r0 + wid + 8 * k;
+    const int64_t row = r0 + wid + FWDT_WAVES * k;
     ss[k] = 0.f;
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) {
@@ -127,7 +132,7 @@ __global__ __launch_bounds__(512) void rmsnorm_fwd_t_kernel(const bf16_t* __rest
   for (int k = 0; k < RPW; ++k) ss[k] = wave_sum(ss[k]);
 #pragma unroll
   for (int k = 0; k < RPW; ++k) {
-    const int lr = wid + 8 * k;
+    const int lr = wid + FWDT_WAVES * k;
     const int64_t row = r0 + lr;
     const float rs = rsqrtf(ss[k] / (float)COLS + eps);
     if (lane == 0) rstd[row] = rs;
@@ -145,7 +150,7 @@ __global__ __launch_bounds__(512) void rmsnorm_fwd_t_kernel(const bf16_t* __rest
   }
   __syncthreads();
   // a task = 2 adjacent columns x 8 tokens: 8 dword LDS reads -> two 16-byte y^T segments
-  for (int task = threadIdx.x; task < COLS * 2; task += 512) {
+  for (int task = threadIdx.x; task < COLS * 2; task += FWDT_WAVES * 64) {
     const int cp = task >> 2, part = task & 3;
     u16x8 o0, o1;
 #pragma unroll
@@ -349,7 +354,7 @@ int pico_rmsnorm_fwd_t(const void* x, const void* residual, const void* weight, 
     hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return pico_set_error("pico_rmsnorm_fwd_t: cannot set LDS size (%d)", (int)e);
     PICO_LAUNCH(PICO_K_RMSNORM_FWD, "rmsnorm_fwd_t", s,
-                k<<<nb, 512, lds, s>>>(xp, rp, wp, (bf16_t*)y, (bf16_t*)residual_out, rstd, (bf16_t*)y_t, ld_t, eps));
+                k<<<nb, FWDT_WAVES * 64, lds, s>>>(xp, rp, wp, (bf16_t*)y, (bf16_t*)residual_out, rstd, (bf16_t*)y_t, ld_t, eps));
     return 0;
   };
   using I2 = std::integral_constant<int, 2>;
