@@ -247,10 +247,15 @@ __global__ __launch_bounds__(NW * 64) void rmsnorm_bwd_kernel(const bf16_t* __re
   }
 }
 
+#ifndef PICO_RMS_BWD_NW4
+#define PICO_RMS_BWD_NW4 8
+#endif
+constexpr int bwd_waves(int maxc) { return maxc <= 2 ? 16 : (maxc == 4 ? PICO_RMS_BWD_NW4 : 4); }
+
 template <int M>
 int launch_rmsnorm_bwd(const void* dy, const void* dres, const void* x, const void* w, const float* rstd, void* dx,
                        float* part, int64_t rows, int c, int nb, hipStream_t s) {
-  constexpr int NW = M <= 2 ? 16 : (M == 4 ? 8 : 4);
+  constexpr int NW = bwd_waves(M);
   auto go = [&](auto full, auto res) {
     PICO_LAUNCH(PICO_K_RMSNORM_BWD, "rmsnorm_bwd", s,
                 (rmsnorm_bwd_kernel<M, NW, decltype(full)::value, decltype(res)::value><<<nb, NW * 64, 0, s>>>(
@@ -313,7 +318,6 @@ int maxc_for(int64_t cols) {
   return -1;
 }
 
-constexpr int bwd_waves(int maxc) { return maxc <= 2 ? 16 : (maxc == 4 ? 8 : 4); }
 
 #ifndef PICO_RMS_BWD_MAXB
 #define PICO_RMS_BWD_MAXB 256
