@@ -76,12 +76,12 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd_kernel(const bf16_t* __restri
 
 // Forward that also writes y^T ([cols, rows], row stride ldt): the x^T the following projection's
 // weight-gradient GEMM reads (TT form), at the cost of one extra write instead of a transpose pass.
-// One 1024-thread workgroup per 32 rows (wave w: rows w, w + 16; a lane owns 8 contiguous columns
+// One 512-thread workgroup per 32 rows (wave w: rows w, w + 8, ...; a lane owns 8 contiguous columns
 // per 512-column chunk as in rmsnorm_fwd_kernel); y is also staged into an LDS tile [32][cols + 8]
 // (128.5 KiB at cols = 2048), then each thread stores 8-token segments of y^T rows (4 x 16 B per
 // 64-B row segment). Requires cols == MAXC * 512 and rows % 32 == 0 (host checks).
 #ifndef PICO_RMS_FWDT_WAVES
-#define PICO_RMS_FWDT_WAVES 16
+#define PICO_RMS_FWDT_WAVES 8
 #endif
 constexpr int FWDT_WAVES = PICO_RMS_FWDT_WAVES;  // waves per 32-row tile (rows per wave = 32 / FWDT_WAVES)
 
