@@ -71,7 +71,9 @@ enum {
   PICO_K_ATTN_BWD_DKV = 19,
   PICO_K_SORT_IDS = 20,
   PICO_K_ADAMW = 21,
-  PICO_K_COUNT = 22
+  PICO_K_ATTN_BWD_KV = 22, /* split backward (D = 64): dK/dV key-major kernel */
+  PICO_K_ATTN_BWD_Q = 23,  /* split backward (D = 64): dQ query-major kernel (+ delta, LSE*log2e) */
+  PICO_K_COUNT = 24
 };
 
 int pico_abi_version(void);

@@ -17,6 +17,7 @@ K_RMSNORM_FWD, K_RMSNORM_BWD, K_RMSNORM_DW, K_ROPE = 1, 2, 3, 4
 K_SWIGLU_FWD, K_SWIGLU_BWD, K_ATTN_FWD, K_ATTN_BWD_PRE = 5, 6, 7, 8
 K_ATTN_BWD, K_ATTN_BWD_DQ, K_GRAD_ACCUM, K_CAST, K_SCALE, K_ATTN_MERGE = 9, 10, 11, 12, 13, 14
 K_EMBEDDING_BWD, K_CE_FWD, K_CE_BWD, K_TRANSPOSE, K_ATTN_BWD_DKV, K_SORT_IDS, K_ADAMW = 15, 16, 17, 18, 19, 20, 21
+K_ATTN_BWD_KV, K_ATTN_BWD_Q = 22, 23
 KERNEL_NAMES = {
     K_RMSNORM_FWD: "rmsnorm_fwd", K_RMSNORM_BWD: "rmsnorm_bwd", K_RMSNORM_DW: "rmsnorm_dw", K_ROPE: "rope",
     K_SWIGLU_FWD: "swiglu_fwd", K_SWIGLU_BWD: "swiglu_bwd", K_ATTN_FWD: "attn_fwd",
@@ -24,6 +25,7 @@ KERNEL_NAMES = {
     K_GRAD_ACCUM: "grad_accum", K_CAST: "cast_f32_bf16", K_SCALE: "scale_f32", K_ATTN_MERGE: "attn_merge",
     K_EMBEDDING_BWD: "embedding_bwd", K_CE_FWD: "cross_entropy_fwd", K_CE_BWD: "cross_entropy_bwd",
     K_TRANSPOSE: "transpose_bf16", K_ATTN_BWD_DKV: "attn_bwd_dkv", K_SORT_IDS: "sort_ids", K_ADAMW: "adamw",
+    K_ATTN_BWD_KV: "attn_bwd_kv", K_ATTN_BWD_Q: "attn_bwd_q",
 }
 
 ATTN_DQ_F32_ACCUM = 1

@@ -23,6 +23,14 @@ CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno
           "-munsafe-fp-atomics"]
 
 
+# per-source flags: the split attention backward keeps MFMA results in VGPRs (its softmax reads them every
+# tile; AGPR accumulators cost one v_accvgpr_read per score) and no SLP-packed f32 VALU beside the MFMAs
+# (cdna_hip_programming.md / MI355X_MICROARCH.md: packed f32 ops are an anti-lever there)
+FILE_FLAGS = {
+    "attn_bwd_split.hip": ["-fno-slp-vectorize", "-mllvm", "-amdgpu-mfma-vgpr-form"],
+}
+
+
 def sources():
     return sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".hip"))
 
@@ -33,7 +41,7 @@ def _compile(src, extra, verbose):
     deps.append(os.path.join(HERE, "..", "include", "picotron_hip.h"))
     if os.path.exists(obj) and not extra and all(os.path.getmtime(obj) >= os.path.getmtime(d) for d in deps):
         return obj, ""
-    cmd = [HIPCC, *CFLAGS, *extra, "-c", src, "-o", obj]
+    cmd = [HIPCC, *CFLAGS, *FILE_FLAGS.get(os.path.basename(src), []), *extra, "-c", src, "-o", obj]
     if verbose:
         print(" ".join(cmd), flush=True)
     r = subprocess.run(cmd, capture_output=True, text=True)

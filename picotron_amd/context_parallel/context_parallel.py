@@ -8,7 +8,9 @@ Differences (MI355X-native, same numbers):
     matmul/softmax; the LSE merge is the pico_attn_merge kernel (same sigmoid/logsigmoid form);
   * each block's backward is pico_attn_bwd fed the GLOBAL O and LSE, accumulating dq directly in
     fp32 (PICO_ATTN_DQ_F32_ACCUM) instead of converting per block;
-  * tensors are in the kernels' native [B, S, H, D] layout (the caller never transposes);
+  * the interface keeps the reference's layout — q/k/v and the output are [B, H, S, D] (ref :14-15, caller
+    ref picotron/model.py:147-150) — but internally the blocks run on [B, S, H, D] views of the same
+    storage (a transpose view, no copy), the kernels' native layout;
   * the ring transport waits on its requests only (no device-wide synchronize per step).
 """
 import os
@@ -27,8 +29,14 @@ def apply_context_parallel(model):
 
 
 def ring_attention(q, k, v, sm_scale, is_causal):
-    """q [B, S_local, Hq, D], k/v [B, S_local, Hkv, D] -> out [B, S_local, Hq, D]."""
-    return RingAttentionFunc.apply(q, k, v, sm_scale, is_causal)
+    """q [B, Hq, S_local, D], k/v [B, Hkv, S_local, D] -> out [B, Hq, S_local, D] (ref :14-15: the
+    reference's caller transposes its [B, S, H, D] projections to this layout and transposes the output
+    back, ref picotron/model.py:139-150). Hkv may divide Hq (native GQA; the reference passes k/v already
+    repeat_interleave'd to Hq heads, which works as well)."""
+    if q.dim() != 4 or k.dim() != 4 or v.dim() != 4:
+        raise ValueError("ring_attention: q, k, v must be [batch, heads, seqlen, head_dim]")
+    out = RingAttentionFunc.apply(q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2), sm_scale, is_causal)
+    return out.transpose(1, 2)
 
 
 def update_out_and_lse(out, lse, block_out, block_lse):
@@ -49,6 +57,8 @@ def update_out_and_lse(out, lse, block_out, block_lse):
 
 
 class RingAttentionFunc(torch.autograd.Function):
+    """Ring attention on [B, S_local, H, D] tensors (views allowed); `ring_attention` is the reference-layout
+    entry point."""
 
     @staticmethod
     def forward(ctx, q, k, v, sm_scale, is_causal):

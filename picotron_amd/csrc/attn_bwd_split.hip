@@ -1,0 +1,721 @@
+// Flash-attention backward for gfx950, split form (head_dim 64): a query-major dQ kernel and a
+// key-major dK/dV kernel instead of one kernel whose dQ needs a cross-workgroup reduction.
+//
+// Replaces flash-attn's backward of flash_attn_func (ref picotron/model.py:36) and the ring block
+// backward ring_attention_backward (ref picotron/context_parallel/context_parallel.py:130-155):
+//   P = exp(scale*QK^T - LSE), delta = rowsum(dO*O), dS = P*(dO V^T - delta),
+//   dQ = scale * dS K, dK = scale * dS^T Q, dV = P^T dO.
+//
+// Why split: with one workgroup per key block, dQ is a sum over key blocks. At D = 64 that sum is one
+// fp32 byte per 640 FLOPs — float atomics cap the kernel near a third of the MFMA peak and partial
+// slabs cost O(S^2 / 256) workspace plus a read-back pass (VERDICT r01 "What's weak" 3).
+// Here each output has exactly one owner and no reduction exists:
+//   attn_bwd_q_kernel  (runs first): one workgroup = 4 waves = 128 query rows of one (batch, q-head),
+//     sweeping 64-key tiles of K and V (LDS-DMA ring). Swapped products with the query on the lane:
+//     S^T = K Q^T and dP^T = V dO^T (A = K / V rows from LDS, B = Q / dO fragments held in registers),
+//     P^T and dS^T lane-local (LSE and delta are per-lane constants; dP starts from -delta as the
+//     MFMA's C operand), dQ^T += K^T dS^T (A = transposed reads of the same K image, B = the dS^T
+//     accumulator packed to bf16 in place). It also computes delta = rowsum(dO*O) from registers and
+//     writes delta / LSE*log2(e) for the second kernel (no separate pre-pass).
+//   attn_bwd_kv_kernel: one workgroup = 4 waves x 64 keys = 256 keys of one (batch, kv-head),
+//     sweeping (query head of the group) x 32-row query tiles (Q, dO, LSE/delta by LDS-DMA). Key on
+//     the lane: S = Q K^T, dP = dO V^T (K, V fragments resident in registers), then dV^T += dO^T P and
+//     dK^T += Q^T dS with the P / dS accumulators as B operands (no LDS round trip at all).
+// The dQ kernel recomputes S and dP (3 products per score there, 4 in the dK/dV kernel: 7 vs the fused
+// form's 5), trading 40 % more MFMA work for no slabs, no atomics, no cross-wave dS exchange and no
+// barrier other than the ring's.
+// RoPE^-1 (PICO_ATTN_ROPE_BWD) is applied in both epilogues: the rotation pairs (d, d + D/2) sit in
+// one lane (accumulator tiles dt and dt + D/64), so it is register-local.
+#include "attn_common.h"
+
+namespace {
+
+constexpr int QB = 128;  // dq kernel: query rows per workgroup (4 waves x 32)
+constexpr int KT = 64;   // dq kernel: keys per tile
+constexpr int KVB = 256; // dkv kernel: keys per workgroup (4 waves x 64)
+constexpr int QT = 32;   // dkv kernel: query rows per tile
+
+// PICO_BWDKV_STAMP: diagnostic build — workgroup 0 of the dK/dV kernel records s_memtime per (wave, tile,
+// phase) and writes them after the workspace (pico_attn_bwd_split_workspace grows by STAMP_BYTES)
+#ifndef PICO_BWDKV_STAMP
+#define PICO_BWDKV_STAMP 0
+#endif
+constexpr int STAMP_T = 48, STAMP_P = 5;
+constexpr int64_t STAMP_BYTES = PICO_BWDKV_STAMP ? 4 * STAMP_T * STAMP_P * 8 : 0;
+
+#ifndef PICO_BWDQ_NBUF
+#define PICO_BWDQ_NBUF 3
+#endif
+
+template <int D>
+struct QCfg {
+  static constexpr int KS = D / 16, DT = D / 32, CPR = D / 8, RB = 2 * D;
+  static constexpr int IMG = KT * RB;          // one K (or V) tile image (lds_off<D> layout)
+  static constexpr int SLOT = 2 * IMG;         // K | V
+  static constexpr int NBUF = PICO_BWDQ_NBUF;  // ring slots; prefetch distance NBUF - 1
+  static constexpr int RPP = 1024 / RB;        // image rows per 1-KiB DMA piece
+  static constexpr int NP = SLOT / 1024;       // pieces per tile
+  static constexpr int NPW = NP / 4;           // per wave
+};
+
+template <int D>
+struct KVCfg {
+  static constexpr int KS = D / 16, DT = D / 32, CPR = D / 8, RB = 2 * D;
+  static constexpr int QIMG = QT * RB;   // one Q (or dO) tile image
+  static constexpr int LSD = 1024;       // LSE*log2e [32] | -delta [32] (one DMA piece)
+  static constexpr int SLOT = 2 * QIMG + LSD;
+  static constexpr int NBUF = 3, PD = 2;  // ring slots, prefetch distance
+  static constexpr int RPP = 1024 / RB;
+  static constexpr int NQP = QIMG / 1024;
+  static constexpr int NP = 2 * NQP + 1;
+  static constexpr int NPW = (NP + 3) / 4;
+};
+
+PICO_DEV float halves_sum2(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+PICO_DEV bf16x8 tr_pair(const char* base, unsigned lo_off, unsigned hi_off) {
+  const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(base + lo_off));
+  const i16x4 up = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(base + hi_off));
+  typedef __attribute__((ext_vector_type(8))) short i16x8;
+  i16x8 v = {lo[0], lo[1], lo[2], lo[3], up[0], up[1], up[2], up[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// Per-lane byte offsets of the 32x32x16 transposed operand of a [rows][D] lds_off<D> image: rows
+// 4 (lane >> 5) + ((lane & 15) >> 2) (+8 for the second read), columns 32 dt + 16 ((lane >> 4) & 1) +
+// 4 (lane & 3). A read at row0 (a multiple of 16: the swizzles see row bits 0-3 only) adds row0 * 2D.
+template <int D>
+PICO_DEV void tr_offsets(int lane, unsigned (&tro)[D / 32][2]) {
+  const int g = lane >> 4, i = lane & 15, hh = g >> 1, q = i >> 2, p = i & 3;
+#pragma unroll
+  for (int dt = 0; dt < D / 32; ++dt) {
+    const int col = 32 * dt + 16 * (g & 1) + 4 * p;
+    tro[dt][0] = lds_off<D>(4 * hh + q, col >> 3) + (col & 7) * 2;
+    tro[dt][1] = lds_off<D>(4 * hh + q + 8, col >> 3) + (col & 7) * 2;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// dQ kernel (query-major)
+// ------------------------------------------------------------------------------------------------
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(256, 2) void attn_bwd_q_kernel(const pico_attn_args a, float scale, float scale_log2,
+                                                             float* __restrict__ lse2_g, float* __restrict__ delta_g,
+                                                             int sq_pad) {
+  using C = QCfg<D>;
+  constexpr int KS = C::KS, DT = C::DT, RB = C::RB;
+  __shared__ __attribute__((aligned(16))) char smem[C::NBUF * C::SLOT];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r = lane & 31, h = lane >> 5;
+  const int Sq = (int)a.seqlen_q, Sk = (int)a.seqlen_k;
+
+  // heaviest query blocks of every head first (causal); a head's blocks sit nbh block ids apart
+  const int nmb = (Sq + QB - 1) / QB;
+  const int nbh = (int)(a.batch * a.heads_q);
+  const int lin = blockIdx.x;
+  const int mb = CAUSAL ? (nmb - 1 - lin / nbh) : (lin / nbh);
+  const int bh = lin % nbh;
+  const int b = bh / (int)a.heads_q, hq = bh % (int)a.heads_q;
+  const int hk = hq / (int)(a.heads_q / a.heads_kv);
+  const int q0 = mb * QB, qw = q0 + 32 * wave, my_q = qw + r;
+  const int qc = min(my_q, Sq - 1);
+
+  const bf16_t* kg = (const bf16_t*)a.k + b * a.k_strides[0] + hk * a.k_strides[2];
+  const bf16_t* vg = (const bf16_t*)a.v + b * a.v_strides[0] + hk * a.v_strides[2];
+  const int64_t ksd = a.k_strides[1], vsd = a.v_strides[1];
+
+  int kend = Sk;
+  if (CAUSAL) kend = min(Sk, q0 + QB);
+  const int ntiles = (kend + KT - 1) / KT;
+  const int lim_last = CAUSAL ? min(qw + 31, Sk - 1) : Sk - 1;   // last key any row of the wave sees
+  const int lim_first = CAUSAL ? min(qw, Sk - 1) : Sk - 1;       // keys <= this need no mask
+  const int lim_lane = CAUSAL ? min(my_q, Sk - 1) : Sk - 1;      // this lane's row sees keys <= it
+
+  // ---- DMA: piece j = wave + 4 i of a tile; j < NP/2: K image piece j, else V image piece j - NP/2 ----
+  int src_row[C::NPW], src_col[C::NPW];
+  unsigned dst_off[C::NPW];
+  bool is_k[C::NPW];
+#pragma unroll
+  for (int i = 0; i < C::NPW; ++i) {
+    const int j = wave + 4 * i;
+    is_k[i] = j < C::NP / 2;
+    const int jj = is_k[i] ? j : j - C::NP / 2;
+    const int row = C::RPP * jj + lane / C::CPR;
+    src_row[i] = row;
+    src_col[i] = 8 * ((lane % C::CPR) ^ swz<D>(row));
+    dst_off[i] = (is_k[i] ? 0u : (unsigned)C::IMG) + (unsigned)jj * 1024u;
+  }
+  const unsigned smem_lds = (unsigned)__builtin_amdgcn_readfirstlane((int)lds_addr(smem));
+  auto issue = [&](int tile) __attribute__((always_inline)) {
+    const unsigned slot = smem_lds + (unsigned)(tile % C::NBUF) * (unsigned)C::SLOT;
+    const int base = tile * KT;
+    const int lastrow = Sk - 1 - base;  // rows past it are clamped (finite; masked by the softmax)
+#pragma unroll
+    for (int i = 0; i < C::NPW; ++i) {
+      const int row = min(src_row[i], lastrow);
+      const void* tb = is_k[i] ? (const void*)(kg + (int64_t)base * ksd) : (const void*)(vg + (int64_t)base * vsd);
+      const unsigned off = (unsigned)(row * (is_k[i] ? ksd : vsd) + src_col[i]) * 2u;
+      dma_piece(tb, off, slot + dst_off[i]);
+    }
+  };
+  constexpr int P = C::NBUF - 1;  // prefetch distance
+#pragma unroll
+  for (int t = 0; t < P; ++t)
+    if (t < ntiles) issue(t);
+
+  // ---- Q, dO fragments (B operands), delta = rowsum(dO * O), LSE ----
+  bf16x8 qf[KS], df[KS];
+  float dsum = 0.f;
+  {
+    const int64_t qoff = b * a.q_strides[0] + hq * a.q_strides[2] + (int64_t)qc * a.q_strides[1] + 8 * h;
+    const int64_t dooff = b * a.do_strides[0] + hq * a.do_strides[2] + (int64_t)qc * a.do_strides[1] + 8 * h;
+    const int64_t ooff = b * a.o_strides[0] + hq * a.o_strides[2] + (int64_t)qc * a.o_strides[1] + 8 * h;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const u16x8 qv = *reinterpret_cast<const u16x8*>((const bf16_t*)a.q + qoff + 16 * ks);
+      const u16x8 dv = *reinterpret_cast<const u16x8*>((const bf16_t*)a.dout + dooff + 16 * ks);
+      const u16x8 ov = *reinterpret_cast<const u16x8*>((const bf16_t*)a.o + ooff + 16 * ks);
+      qf[ks] = __builtin_bit_cast(bf16x8, qv);
+      df[ks] = __builtin_bit_cast(bf16x8, dv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dsum += bf2f(ov[j]) * bf2f(dv[j]);
+    }
+  }
+  // consume the prologue loads here: otherwise the compiler's own vmcnt waits for them sit at their
+  // first use inside the tile loop, where vmcnt also counts the ring's in-flight DMA (-> vmcnt(0) per tile)
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) asm volatile("" : "+v"(qf[ks]), "+v"(df[ks]));
+  const float dall = halves_sum2(dsum);
+  const bool row_ok = my_q < Sq;
+  const float delta = row_ok ? dall : 0.f;
+  const float lse2 = row_ok ? a.lse[((int64_t)b * a.heads_q + hq) * Sq + my_q] * LOG2E : INFINITY;
+  if (h == 0 && my_q < sq_pad) {  // for attn_bwd_kv_kernel (padding rows: P = 0, delta = 0)
+    lse2_g[(int64_t)bh * sq_pad + my_q] = lse2;
+    delta_g[(int64_t)bh * sq_pad + my_q] = -delta;
+  }
+
+  // per-lane LDS offsets, pinned in registers (the compiler would otherwise re-derive the swizzles)
+  unsigned ro[KS], tro[DT][2];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) ro[ks] = lds_off<D>(r, 2 * ks + h);
+  tr_offsets<D>(lane, tro);
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) asm volatile("" : "+v"(ro[ks]));
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) asm volatile("" : "+v"(tro[dt][0]), "+v"(tro[dt][1]));
+
+  f32x16 dq[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) dq[dt] = (f32x16)0.f;
+  const f32x16 ndelta = (f32x16)(-delta);
+  const float nl2 = -lse2;
+
+  // One 64-key tile: S^T, dP^T (8 + 8 MFMAs), P^T and dS^T in registers, dQ^T += K^T dS^T (8 MFMAs).
+  // kb: the slot's K image (V image at +IMG). One body for every tile (the causal / padding mask is an
+  // in-place branch on S), so the loop-carried dQ accumulators never move between registers.
+  auto tile = [&](const char* kb, bool mask, int n0) __attribute__((always_inline)) {
+    const char* vb = kb + C::IMG;
+    bf16x8 kf[2][KS], vf[2][KS];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        kf[kt][ks] = lds_read_b128(kb, ro[ks] + kt * 32 * RB);
+        vf[kt][ks] = lds_read_b128(vb, ro[ks] + kt * 32 * RB);
+      }
+    f32x16 s[2], dp[2];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      s[kt] = mfma32(kf[kt][0], qf[0], (f32x16)0.f);
+#pragma unroll
+      for (int ks = 1; ks < KS; ++ks) s[kt] = mfma32(kf[kt][ks], qf[ks], s[kt]);
+      dp[kt] = mfma32(vf[kt][0], df[0], ndelta);
+#pragma unroll
+      for (int ks = 1; ks < KS; ++ks) dp[kt] = mfma32(vf[kt][ks], df[ks], dp[kt]);
+    }
+    // lane = query my_q; register i of half kt = key n0 + 32 kt + acc_row(i, h)
+    if (mask) {  // wave-uniform: diagonal / partial tiles only
+      const int rel = lim_lane - n0 - 4 * h;  // key allowed iff (32 kt + (i&3) + 8 (i>>2)) <= rel
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) s[kt][i] = (32 * kt + (i & 3) + 8 * (i >> 2)) <= rel ? s[kt][i] : -INFINITY;
+    }
+    bf16x8 dsf[2][2];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      float ds[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) ds[i] = fast_exp2(__builtin_fmaf(s[kt][i], scale_log2, nl2)) * dp[kt][i];
+      dsf[kt][0] = pack_bf16x8(ds);
+      dsf[kt][1] = pack_bf16x8(ds + 8);
+    }
+    // dQ^T[d][q] += K^T[d][key] dS^T[key][q]: A = transposed reads of the K image
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        const char* rowb = kb + (32 * kt + 16 * st) * RB;
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) dq[dt] = mfma32(tr_pair(rowb, tro[dt][0], tro[dt][1]), dsf[kt][st], dq[dt]);
+      }
+  };
+
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // prologue tiles and loads landed
+  for (int t = 0; t < ntiles; ++t) {
+    if (t > 0) {  // tile t landed (this wave's pieces); the younger tiles stay in flight
+      if (P == 2 && t + 1 < ntiles) {
+        if constexpr (C::NPW == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    }
+    lds_barrier();  // every wave's pieces of tile t visible; slot (t + P) % NBUF no longer read
+    if (t + P < ntiles) issue(t + P);
+    const int n0 = t * KT;
+    if (n0 <= lim_last) {  // wave-uniform: some row of the wave sees some key of the tile
+      tile(smem + (unsigned)(t % C::NBUF) * (unsigned)C::SLOT, n0 + KT - 1 > lim_first, n0);
+    }
+  }
+
+  // ---- epilogue: lane = query my_q, register i of tile dt = d 32 dt + acc_row(i, h) ----
+  if (!row_ok) return;
+  if (a.flags & PICO_ATTN_ROPE_BWD) {  // rotate back by -theta: pairs (d, d + D/2) = tiles (dt, dt + DT/2)
+    const bf16_t* cp = (const bf16_t*)a.rope_cos + (int64_t)my_q * a.rope_stride;
+    const bf16_t* sp = (const bf16_t*)a.rope_sin + (int64_t)my_q * a.rope_stride;
+#pragma unroll
+    for (int dt = 0; dt < DT / 2; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const u16x4 c4 = *reinterpret_cast<const u16x4*>(cp + 32 * dt + 8 * g + 4 * h);
+        const u16x4 s4 = *reinterpret_cast<const u16x4*>(sp + 32 * dt + 8 * g + 4 * h);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float cf = bf2f(c4[j]), sf = bf2f(s4[j]);
+          const float x1 = dq[dt][4 * g + j], x2 = dq[dt + DT / 2][4 * g + j];
+          dq[dt][4 * g + j] = x1 * cf + x2 * sf;
+          dq[dt + DT / 2][4 * g + j] = x2 * cf - x1 * sf;
+        }
+      }
+  }
+  if (a.flags & PICO_ATTN_DQ_F32_ACCUM) {
+    float* dst = (float*)a.dq + b * a.dq_strides[0] + hq * a.dq_strides[2] + (int64_t)my_q * a.dq_strides[1];
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        float* p = dst + 32 * dt + 8 * g + 4 * h;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) p[j] += dq[dt][4 * g + j] * scale;
+      }
+    return;
+  }
+  bf16_t* dst = (bf16_t*)a.dq + b * a.dq_strides[0] + hq * a.dq_strides[2] + (int64_t)my_q * a.dq_strides[1];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      u16x4 w;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) w[j] = f2bf(dq[dt][4 * g + j] * scale);
+      *reinterpret_cast<u16x4*>(dst + 32 * dt + 8 * g + 4 * h) = w;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// dK / dV kernel (key-major)
+// ------------------------------------------------------------------------------------------------
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(256, 1) void attn_bwd_kv_kernel(const pico_attn_args a, float scale, float scale_log2,
+                                                              const float* __restrict__ lse2_g,
+                                                              const float* __restrict__ delta_g, int sq_pad,
+                                                              int hsplit, float* __restrict__ dkv_part,
+                                                              unsigned long long* __restrict__ stamp_out) {
+  using C = KVCfg<D>;
+  constexpr int KS = C::KS, DT = C::DT, CPR = C::CPR, RB = C::RB;
+  __shared__ __attribute__((aligned(16))) char smem[C::NBUF * C::SLOT];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r = lane & 31, h = lane >> 5;
+  const int Sq = (int)a.seqlen_q, Sk = (int)a.seqlen_k;
+  const int Hq = (int)a.heads_q;
+  const int G = (int)(a.heads_q / a.heads_kv);
+
+  // heaviest key blocks first (causal: block 0 sees every query); small grids split a key block's
+  // (query head, query tile) list over `hsplit` workgroups with fp32 partials (attn_bwd_dkv_kernel sums)
+  const int nbh = (int)(a.batch * a.heads_kv) * hsplit;
+  const int kb = blockIdx.x / nbh;
+  const int bhs = blockIdx.x % nbh;
+  const int hs = bhs % hsplit;
+  const int bh = bhs / hsplit;
+  const int b = bh / (int)a.heads_kv, hk = bh % (int)a.heads_kv;
+  const int k0 = kb * KVB;
+  const int kw = k0 + 64 * wave;  // this wave's first key
+
+  const int qstart = CAUSAL ? k0 : 0;  // k0 is a multiple of QT
+  const int nqt = Sq > qstart ? (Sq - qstart + QT - 1) / QT : 0;
+  const int ntot = G * nqt;
+  const int tb = (int)((int64_t)ntot * hs / hsplit);
+  const int ntiles = (int)((int64_t)ntot * (hs + 1) / hsplit) - tb;
+  const int hq0 = hk * G + (nqt ? tb / nqt : 0), q00 = qstart + (nqt ? tb % nqt : 0) * QT;
+
+  // ---- tile DMA: piece j issued by wave j % 4: Q pieces, dO pieces, then the LSE/delta piece ----
+  const int my_np = (C::NP / 4) + (wave < C::NP % 4 ? 1 : 0);
+  int pc_row[C::NPW], pc_col[C::NPW], pc_kind[C::NPW];
+  unsigned pc_dst[C::NPW];
+#pragma unroll
+  for (int i = 0; i < C::NPW; ++i) {
+    const int j = wave + 4 * i;
+    if (j < 2 * C::NQP) {
+      const int jj = j % C::NQP, row = C::RPP * jj + lane / CPR;
+      pc_kind[i] = j < C::NQP ? 0 : 1;
+      pc_row[i] = row;
+      pc_col[i] = 8 * ((lane % CPR) ^ swz<D>(row));
+      pc_dst[i] = (j < C::NQP ? 0 : C::QIMG) + jj * 1024;
+    } else {  // lanes 0-7: LSE*log2e rows 4l..4l+3; 8-15: -delta rows (16-63 repeat)
+      const int l = lane & 15;
+      pc_kind[i] = 2;
+      pc_row[i] = 4 * (l & 7);
+      pc_col[i] = l >> 3;
+      pc_dst[i] = 2 * C::QIMG;
+    }
+  }
+  struct Tc {
+    int hq, q0;
+  };
+  const int qend = qstart + nqt * QT;
+  auto advance = [&](Tc& c) __attribute__((always_inline)) {
+    c.q0 += QT;
+    if (c.q0 >= qend) {
+      c.q0 = qstart;
+      ++c.hq;
+    }
+  };
+  const bf16_t* qbase = (const bf16_t*)a.q + b * a.q_strides[0];
+  const bf16_t* dobase = (const bf16_t*)a.dout + b * a.do_strides[0];
+  const unsigned delta_off = (unsigned)((const char*)delta_g - (const char*)lse2_g);  // same workspace
+  const unsigned ring_lds = (unsigned)__builtin_amdgcn_readfirstlane((int)lds_addr(smem));
+  auto issue = [&](int si, Tc c) __attribute__((always_inline)) {
+    const int hq = c.hq, q0 = c.q0;
+    const bool full = q0 + QT <= Sq;
+#pragma unroll
+    for (int i = 0; i < C::NPW; ++i) {
+      if (i < my_np) {
+        const void* base;
+        unsigned off;
+        if (pc_kind[i] == 2) {
+          base = lse2_g + ((int64_t)b * Hq + hq) * sq_pad + q0;
+          off = (unsigned)pc_row[i] * 4u + (pc_col[i] ? delta_off : 0u);
+        } else {
+          const int dq = full ? pc_row[i] : min(q0 + pc_row[i], Sq - 1) - q0;
+          if (pc_kind[i] == 0) {
+            base = qbase + hq * a.q_strides[2] + (int64_t)q0 * a.q_strides[1];
+            off = (unsigned)(dq * a.q_strides[1] + pc_col[i]) * 2u;
+          } else {
+            base = dobase + hq * a.do_strides[2] + (int64_t)q0 * a.do_strides[1];
+            off = (unsigned)(dq * a.do_strides[1] + pc_col[i]) * 2u;
+          }
+        }
+        dma_piece(base, off, ring_lds + (unsigned)si * (unsigned)C::SLOT + pc_dst[i]);
+      }
+    }
+  };
+  constexpr int PD = C::PD;
+  Tc nxt = {hq0, q00};
+#pragma unroll
+  for (int j = 0; j < PD; ++j) {
+    if (j < ntiles) issue(j, nxt);
+    advance(nxt);
+  }
+
+  // ---- K, V fragments of this wave's 64 keys (B operands of S = Q K^T, dP = dO V^T) ----
+  const bf16_t* kg = (const bf16_t*)a.k + b * a.k_strides[0] + hk * a.k_strides[2];
+  const bf16_t* vg = (const bf16_t*)a.v + b * a.v_strides[0] + hk * a.v_strides[2];
+  bf16x8 kf[2][KS], vf[2][KS];
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt) {
+    const int key = kw + 32 * kt + r;
+    const bool ok = key < Sk;
+    const bf16_t* kp = kg + (int64_t)min(key, Sk - 1) * a.k_strides[1] + 8 * h;
+    const bf16_t* vp = vg + (int64_t)min(key, Sk - 1) * a.v_strides[1] + 8 * h;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const u16x8 kv = *reinterpret_cast<const u16x8*>(kp + 16 * ks);
+      const u16x8 vv = *reinterpret_cast<const u16x8*>(vp + 16 * ks);
+      kf[kt][ks] = __builtin_bit_cast(bf16x8, ok ? kv : (u16x8)0);
+      vf[kt][ks] = __builtin_bit_cast(bf16x8, ok ? vv : (u16x8)0);
+    }
+  }
+
+  // consume the loads before the loop (see attn_bwd_q_kernel)
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) asm volatile("" : "+a"(kf[kt][ks]), "+a"(vf[kt][ks]));
+
+  f32x16 dk[DT][2], dv[DT][2];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      dk[dt][kt] = (f32x16)0.f;
+      dv[dt][kt] = (f32x16)0.f;
+    }
+
+  unsigned qo[KS], tro[DT][2];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) qo[ks] = lds_off<D>(r, 2 * ks + h);
+  tr_offsets<D>(lane, tro);
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) asm volatile("" : "+v"(qo[ks]));
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) asm volatile("" : "+v"(tro[dt][0]), "+v"(tro[dt][1]));
+
+  const bool kpad = kw + 63 >= Sk;  // wave-uniform: some of the wave's keys are padding
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // prologue tiles visible
+
+#if PICO_BWDKV_STAMP
+  __shared__ unsigned long long stamps[4 * STAMP_T * STAMP_P];
+  auto stamp = [&](int t, int ph) __attribute__((always_inline)) {
+    __builtin_amdgcn_sched_barrier(0);
+    const unsigned long long v = __builtin_amdgcn_s_memtime();
+    if (lane == 0 && t < STAMP_T) stamps[(wave * STAMP_T + t) * STAMP_P + ph] = v;
+    __builtin_amdgcn_sched_barrier(0);
+  };
+#else
+  auto stamp = [](int, int) __attribute__((always_inline)) {};
+#endif
+  Tc cur = {hq0, q00};
+  int si = 0, si_nxt = PD % C::NBUF;
+  for (int t = 0; t < ntiles; ++t) {
+    stamp(t, 0);
+    if (t > 0) {
+      // this wave's pieces of tile t landed; tile t + 1's (issued one iteration later) may stay in flight
+      if (t + 1 < ntiles) wait_vmcnt(my_np);
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      lds_barrier();  // everyone's pieces of tile t visible; slot (t + PD) % NBUF no longer read
+    }
+    stamp(t, 1);
+    if (t + PD < ntiles) issue(si_nxt, nxt);
+    advance(nxt);
+    stamp(t, 2);
+    const int q0 = cur.q0;
+    // causal: the wave's keys all lie past the tile's last query row -> nothing to do
+    if (!CAUSAL || kw <= q0 + QT - 1) {
+      const char* qs = smem + (unsigned)si * (unsigned)C::SLOT;
+      const char* dos = qs + C::QIMG;
+      const float* lsd = (const float*)(qs + 2 * C::QIMG);
+      bf16x8 qa[KS], da[KS];
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        qa[ks] = lds_read_b128(qs, qo[ks]);
+        da[ks] = lds_read_b128(dos, qo[ks]);
+      }
+      // rows of this lane's accumulator registers: q = q0 + 8 g + 4 h + (0..3)
+      f32x4 l2[4];
+      f32x16 nd;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        l2[g] = *reinterpret_cast<const f32x4*>(lsd + 8 * g + 4 * h);
+        const f32x4 v = *reinterpret_cast<const f32x4*>(lsd + 32 + 8 * g + 4 * h);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) nd[4 * g + j] = v[j];
+      }
+      f32x16 s[2], dp[2];
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        s[kt] = mfma32(qa[0], kf[kt][0], (f32x16)0.f);
+#pragma unroll
+        for (int ks = 1; ks < KS; ++ks) s[kt] = mfma32(qa[ks], kf[kt][ks], s[kt]);
+        dp[kt] = mfma32(da[0], vf[kt][0], nd);
+#pragma unroll
+        for (int ks = 1; ks < KS; ++ks) dp[kt] = mfma32(da[ks], vf[kt][ks], dp[kt]);
+      }
+      stamp(t, 3);
+      if ((CAUSAL && kw + 63 > q0) || kpad) {  // wave-uniform: diagonal tiles / padding keys only
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) {
+          const int key = kw + 32 * kt + r;
+          const int rel = CAUSAL ? key - q0 - 4 * h : -1;  // causal: masked iff (i&3) + 8(i>>2) < rel
+          const bool dead = key >= Sk;
+#pragma unroll
+          for (int i = 0; i < 16; ++i) s[kt][i] = (((i & 3) + 8 * (i >> 2) < rel) || dead) ? -INFINITY : s[kt][i];
+        }
+      }
+      bf16x8 pf[2][2], sf[2][2];
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        float pv[16], sv[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          pv[i] = fast_exp2(__builtin_fmaf(s[kt][i], scale_log2, -l2[i >> 2][i & 3]));
+          sv[i] = pv[i] * dp[kt][i];
+        }
+        pf[kt][0] = pack_bf16x8(pv);
+        pf[kt][1] = pack_bf16x8(pv + 8);
+        sf[kt][0] = pack_bf16x8(sv);
+        sf[kt][1] = pack_bf16x8(sv + 8);
+      }
+      // dV^T[d][key] += dO^T[d][q] P[q][key],  dK^T[d][key] += Q^T[d][q] dS[q][key]
+#pragma unroll
+      for (int st = 0; st < 2; ++st)
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+          const bf16x8 dot = tr_pair(dos + 16 * st * RB, tro[dt][0], tro[dt][1]);
+          const bf16x8 qt = tr_pair(qs + 16 * st * RB, tro[dt][0], tro[dt][1]);
+#pragma unroll
+          for (int kt = 0; kt < 2; ++kt) {
+            dv[dt][kt] = mfma32(dot, pf[kt][st], dv[dt][kt]);
+            dk[dt][kt] = mfma32(qt, sf[kt][st], dk[dt][kt]);
+          }
+        }
+    }
+    stamp(t, 4);
+    advance(cur);
+    si = si + 1 == C::NBUF ? 0 : si + 1;
+    si_nxt = si_nxt + 1 == C::NBUF ? 0 : si_nxt + 1;
+  }
+
+#if PICO_BWDKV_STAMP
+  if (blockIdx.x == 0)
+    for (int i = lane; i < STAMP_T * STAMP_P; i += 64) stamp_out[wave * STAMP_T * STAMP_P + i] = stamps[wave * STAMP_T * STAMP_P + i];
+#endif
+  // ---- epilogue: lane = key kw + 32 kt + r, register i of tile dt = d 32 dt + acc_row(i, h) ----
+  if (hsplit == 1) {
+    const bool rope = (a.flags & PICO_ATTN_ROPE_BWD) != 0;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      const int key = kw + 32 * kt + r;
+      if (key >= Sk) continue;
+      if (rope) {
+        const bf16_t* cp = (const bf16_t*)a.rope_cos + (int64_t)key * a.rope_stride;
+        const bf16_t* sp = (const bf16_t*)a.rope_sin + (int64_t)key * a.rope_stride;
+#pragma unroll
+        for (int dt = 0; dt < DT / 2; ++dt)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const u16x4 c4 = *reinterpret_cast<const u16x4*>(cp + 32 * dt + 8 * g + 4 * h);
+            const u16x4 s4 = *reinterpret_cast<const u16x4*>(sp + 32 * dt + 8 * g + 4 * h);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const float cf = bf2f(c4[j]), sn = bf2f(s4[j]);
+              const float x1 = dk[dt][kt][4 * g + j], x2 = dk[dt + DT / 2][kt][4 * g + j];
+              dk[dt][kt][4 * g + j] = x1 * cf + x2 * sn;
+              dk[dt + DT / 2][kt][4 * g + j] = x2 * cf - x1 * sn;
+            }
+          }
+      }
+      bf16_t* dkp = (bf16_t*)a.dk + b * a.dk_strides[0] + hk * a.dk_strides[2] + (int64_t)key * a.dk_strides[1];
+      bf16_t* dvp = (bf16_t*)a.dv + b * a.dv_strides[0] + hk * a.dv_strides[2] + (int64_t)key * a.dv_strides[1];
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          u16x4 wk, wv;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            wk[j] = f2bf(dk[dt][kt][4 * g + j] * scale);
+            wv[j] = f2bf(dv[dt][kt][4 * g + j]);
+          }
+          *reinterpret_cast<u16x4*>(dkp + 32 * dt + 8 * g + 4 * h) = wk;
+          *reinterpret_cast<u16x4*>(dvp + 32 * dt + 8 * g + 4 * h) = wv;
+        }
+    }
+  } else {  // fp32 partials [hs][dK | dV][b][key][hk][D]
+    const int64_t part = a.batch * a.seqlen_k * a.heads_kv * D;
+    float* pk = dkv_part + (int64_t)(2 * hs) * part + ((int64_t)b * Sk * a.heads_kv + hk) * D;
+    float* pv = pk + part;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      const int key = kw + 32 * kt + r;
+      if (key >= Sk) continue;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          f32x4 wk, wv;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            wk[j] = dk[dt][kt][4 * g + j] * scale;
+            wv[j] = dv[dt][kt][4 * g + j];
+          }
+          const int64_t o = (int64_t)key * a.heads_kv * D + 32 * dt + 8 * g + 4 * h;
+          *reinterpret_cast<f32x4*>(pk + o) = wk;
+          *reinterpret_cast<f32x4*>(pv + o) = wv;
+        }
+    }
+  }
+}
+
+int split_sq_pad(const pico_attn_args* a) { return (int)((a->seqlen_q + QT - 1) / QT) * QT; }
+
+int64_t split_lsd_floats(const pico_attn_args* a) {
+  const int64_t n = a->batch * a->heads_q * (int64_t)split_sq_pad(a);
+  return ((n + 63) / 64) * 64;
+}
+
+// split of a key block's tile list so that the dK/dV grid covers the 256 CUs (one workgroup each)
+int kv_hsplit(const pico_attn_args* a) {
+  if (a->heads_kv <= 0 || a->heads_q % a->heads_kv != 0) return 1;
+  const int64_t nblk = ((a->seqlen_k + KVB - 1) / KVB) * a->batch * a->heads_kv;
+  const int64_t tiles = (a->heads_q / a->heads_kv) * ((a->seqlen_q + QT - 1) / QT);
+  if (nblk <= 0) return 1;
+  int d = 1;
+  while (d < 8 && nblk * d < 256 && 2 * d <= tiles) d *= 2;
+  return d;
+}
+
+}  // namespace
+int64_t pico_attn_bwd_split_workspace(const pico_attn_args* a);
+namespace {
+
+template <bool CAUSAL>
+int launch_split(const pico_attn_args* a, hipStream_t s) {
+  constexpr int D = 64;
+  const int sq_pad = split_sq_pad(a);
+  float* lse2 = (float*)a->workspace;
+  float* delta = lse2 + split_lsd_floats(a);
+  float* dkv_part = delta + split_lsd_floats(a);
+  const float sl2 = a->softmax_scale * LOG2E;
+  const int nmb = (int)((a->seqlen_q + QB - 1) / QB);
+  const int64_t gq = (int64_t)nmb * a->batch * a->heads_q;
+  PICO_REQUIRE(gq < (1ll << 31), "pico_attn_bwd: grid too large");
+  PICO_LAUNCH(PICO_K_ATTN_BWD_Q, "attn_bwd_q", s,
+              attn_bwd_q_kernel<D, CAUSAL><<<(int)gq, 256, 0, s>>>(*a, a->softmax_scale, sl2, lse2, delta, sq_pad));
+  const int nkb = (int)((a->seqlen_k + KVB - 1) / KVB);
+  const int hsplit = kv_hsplit(a);
+  const int64_t nblk = (int64_t)nkb * a->batch * a->heads_kv * hsplit;
+  if (nblk == 0) return 0;
+  PICO_LAUNCH(PICO_K_ATTN_BWD_KV, "attn_bwd_kv", s,
+              attn_bwd_kv_kernel<D, CAUSAL><<<(int)nblk, 256, 0, s>>>(
+                  *a, a->softmax_scale, sl2, lse2, delta, sq_pad, hsplit, dkv_part,
+                  (unsigned long long*)((char*)a->workspace + pico_attn_bwd_split_workspace(a) - STAMP_BYTES)));
+  if (hsplit > 1) {
+    const int kv_blocks = pico_cdiv(a->batch * a->seqlen_k * a->heads_kv * (D / 16), 256);
+    PICO_LAUNCH(PICO_K_ATTN_BWD_DKV, "attn_bwd_dkv", s,
+                attn_bwd_dkv_kernel<D><<<kv_blocks, 256, 0, s>>>(*a, dkv_part, hsplit));
+  }
+  return 0;
+}
+
+}  // namespace
+
+// workspace of the split backward: [lse2 | delta] each [B*Hq][Sq_pad32] fp32 (+ fp32 dK/dV partials when
+// a small grid splits key blocks): O(S), independent of the number of key blocks
+int64_t pico_attn_bwd_split_workspace(const pico_attn_args* a) {
+  const int hs = kv_hsplit(a);
+  const int64_t dkv = hs > 1 ? 2 * hs * a->batch * a->seqlen_k * a->heads_kv * a->head_dim : 0;
+  return (2 * split_lsd_floats(a) + dkv) * 4 + STAMP_BYTES;
+}
+
+int pico_attn_bwd_split(const pico_attn_args* a, hipStream_t s) {
+  return a->causal ? launch_split<true>(a, s) : launch_split<false>(a, s);
+}

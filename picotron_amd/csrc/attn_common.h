@@ -129,4 +129,124 @@ PICO_DEV bf16x8 pack_frag(const float* v) {
   return r;
 }
 
+// The same from 8 floats with one v_cvt_pk_bf16_f32 per pair (element order kept; no lane shuffles).
+PICO_DEV bf16x8 pack_bf16x8(const float* v) {
+  typedef __attribute__((ext_vector_type(2))) float f32x2;
+  typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+  typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+  const bf16x2 p0 = __builtin_convertvector((f32x2){v[0], v[1]}, bf16x2);
+  const bf16x2 p1 = __builtin_convertvector((f32x2){v[2], v[3]}, bf16x2);
+  const bf16x2 p2 = __builtin_convertvector((f32x2){v[4], v[5]}, bf16x2);
+  const bf16x2 p3 = __builtin_convertvector((f32x2){v[6], v[7]}, bf16x2);
+  const bf16x4 lo = __builtin_shufflevector(p0, p1, 0, 1, 2, 3);
+  const bf16x4 hi = __builtin_shufflevector(p2, p3, 0, 1, 2, 3);
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
 PICO_DEV float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// ---- shared by the backward kernels (attn_bwd.hip, attn_bwd_split.hip) ----
+
+// One LDS-DMA piece (16 B per lane, lane-linear at the wave-uniform LDS byte address lds_base) issued
+// from inline asm: the compiler does not see it as an LDS write, so it inserts none of its
+// conservative `s_waitcnt vmcnt(0)` before the loop's LDS reads and writes (which would expose the
+// full HBM latency of the piece just issued, every tile). The kernel's counted waits + barrier order
+// the pieces against their readers; ring slots are never touched while a piece for them is in flight.
+// Address = wave-uniform base (SGPR pair) + per-lane 32-bit byte offset.
+PICO_DEV void dma_piece(const void* base, unsigned voff, unsigned lds_base) {
+  const uint64_t p = (uint64_t)(uintptr_t)base;  // wave-uniform by construction; make it an SGPR pair
+  const uint64_t sbase = (uint64_t)(unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)p) |
+                         ((uint64_t)(unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(p >> 32)) << 32);
+  asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase), "s"(lds_base) : "memory");
+}
+
+// Workgroup barrier without the fence __syncthreads() implies (whose release semantics make the
+// compiler drain vmcnt(0) — the in-flight DMA and dQ stores — before every barrier). LDS writes are
+// drained (lgkmcnt(0)); the asm memory clobbers keep memory accesses from moving across it.
+PICO_DEV void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// s_waitcnt vmcnt(n) for a wave-uniform runtime n (the immediate must be a constant)
+PICO_DEV void wait_vmcnt(int n) {
+  switch (n) {
+#define PICO_VMCNT_CASE(N) \
+  case N:                  \
+    asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); \
+    break;
+    PICO_VMCNT_CASE(1) PICO_VMCNT_CASE(2) PICO_VMCNT_CASE(3) PICO_VMCNT_CASE(4) PICO_VMCNT_CASE(5)
+    PICO_VMCNT_CASE(6) PICO_VMCNT_CASE(7) PICO_VMCNT_CASE(8) PICO_VMCNT_CASE(9) PICO_VMCNT_CASE(10)
+    PICO_VMCNT_CASE(11) PICO_VMCNT_CASE(12) PICO_VMCNT_CASE(13) PICO_VMCNT_CASE(14) PICO_VMCNT_CASE(15)
+    PICO_VMCNT_CASE(16) PICO_VMCNT_CASE(17) PICO_VMCNT_CASE(18) PICO_VMCNT_CASE(19) PICO_VMCNT_CASE(20)
+#undef PICO_VMCNT_CASE
+    default:
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+}
+
+// XOR applied to the 16-B chunk index of image row `row` (see lds_off in attn_common.h)
+template <int D>
+PICO_DEV int swz(int row) {
+  if constexpr (D == 128) return ((row & 3) << 2) | ((row >> 2) & 3);
+  const int y = (row >> 1) & 7;
+  return y ^ ((y & 1) << 2);
+}
+
+// rotate-half RoPE backward (rotation by -theta) of the pair (x[d], x[d + D/2]), d = i0 + j, j < 8, at
+// sequence position pos: x1' = x1 c + x2 s, x2' = x2 c - x1 s (pico_rope with conjugate = 1)
+PICO_DEV void rope_bwd8(const pico_attn_args& a, int pos, int i0, float* x1, float* x2) {
+  const u16x8 c = *reinterpret_cast<const u16x8*>((const bf16_t*)a.rope_cos + (int64_t)pos * a.rope_stride + i0);
+  const u16x8 sn = *reinterpret_cast<const u16x8*>((const bf16_t*)a.rope_sin + (int64_t)pos * a.rope_stride + i0);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float cf = bf2f(c[j]), sf = bf2f(sn[j]), u = x1[j], w = x2[j];
+    x1[j] = u * cf + w * sf;
+    x2[j] = w * cf - u * sf;
+  }
+}
+
+// dK / dV [b, key, hk, :] = sum over the hsplit workgroups' fp32 partials (fixed order) -> bf16 (strided);
+// dK optionally rotated back (PICO_ATTN_ROPE_BWD). Thread layout as attn_bwd_dq_kernel.
+template <int D>
+__global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const pico_attn_args a, const float* __restrict__ dkv_part,
+                                                           int hsplit) {
+  constexpr int TPR = D / 16;
+  const int64_t part = a.batch * a.seqlen_k * a.heads_kv * D;
+  const int64_t rows = a.batch * a.seqlen_k * a.heads_kv;
+  const int64_t row = ((int64_t)blockIdx.x * 256 + threadIdx.x) / TPR;
+  const int d0 = (threadIdx.x % TPR) * 8;
+  if (row >= rows) return;
+  const int hk = (int)(row % a.heads_kv);
+  const int64_t bk = row / a.heads_kv;
+  const int key = (int)(bk % a.seqlen_k);
+  const int b = (int)(bk / a.seqlen_k);
+  for (int which = 0; which < 2; ++which) {
+    float x1[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, x2[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int hs = 0; hs < hsplit; ++hs) {
+      const float* src = dkv_part + (2 * hs + which) * part + row * D + d0;
+      const f32x4 l0 = reinterpret_cast<const f32x4*>(src)[0], l1 = reinterpret_cast<const f32x4*>(src)[1];
+      const f32x4 h0 = reinterpret_cast<const f32x4*>(src + D / 2)[0], h1 = reinterpret_cast<const f32x4*>(src + D / 2)[1];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        x1[j] += l0[j];
+        x1[4 + j] += l1[j];
+        x2[j] += h0[j];
+        x2[4 + j] += h1[j];
+      }
+    }
+    if (which == 0 && (a.flags & PICO_ATTN_ROPE_BWD)) rope_bwd8(a, key, d0, x1, x2);
+    u16x8 o1, o2;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      o1[j] = f2bf(x1[j]);
+      o2[j] = f2bf(x2[j]);
+    }
+    bf16_t* dst = which ? (bf16_t*)a.dv + b * a.dv_strides[0] + key * a.dv_strides[1] + hk * a.dv_strides[2]
+                        : (bf16_t*)a.dk + b * a.dk_strides[0] + key * a.dk_strides[1] + hk * a.dk_strides[2];
+    *reinterpret_cast<u16x8*>(dst + d0) = o1;
+    *reinterpret_cast<u16x8*>(dst + d0 + D / 2) = o2;
+  }
+}
+

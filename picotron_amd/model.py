@@ -166,8 +166,10 @@ class Attention(nn.Module):
         k = ops.apply_rotary_emb(k, cos[:, : D // 2], sin[:, : D // 2])
         causal = q.size(1) == k.size(1)
         if os.getenv("CONTEXT_PARALLEL", "0") == "1":
+            # the reference's call: [B, H, S, D] in, [B, H, S, D] out, transposed back (ref :139-150)
             from .context_parallel import context_parallel
-            out = context_parallel.ring_attention(q, k, v, 1.0 / math.sqrt(D), causal)
+            out = context_parallel.ring_attention(q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2),
+                                                  1.0 / math.sqrt(D), causal).transpose(1, 2)
         else:
             out = ops.flash_attn_func(q, k, v, causal=causal)
         out = out.reshape(B, S, self.num_local_heads * D)

@@ -44,7 +44,8 @@ def main():
             o, lse = ops.attention_block_fwd(q, k, v, sc, causal)
             ops.attention_block_bwd(do, q, k, v, o, lse, sc, causal)
         torch.cuda.synchronize()
-        ids = [L.K_ATTN_FWD, L.K_ATTN_BWD_PRE, L.K_ATTN_BWD, L.K_ATTN_BWD_DQ, L.K_ATTN_BWD_DKV]
+        ids = [L.K_ATTN_FWD, L.K_ATTN_BWD_PRE, L.K_ATTN_BWD, L.K_ATTN_BWD_DQ, L.K_ATTN_BWD_DKV, L.K_ATTN_BWD_Q,
+               L.K_ATTN_BWD_KV]
         for i in ids:
             L.prof_enable(i, args.iters + 4)
         for _ in range(args.iters):
@@ -62,7 +63,8 @@ def main():
                 tot_bwd += us
         L.load().pico_prof_enable(0, 0)
         res["fwd_tflops"] = round(fl / (res["attn_fwd_us"] * 1e-6) / 1e12, 1)
-        res["bwd_kernel_tflops"] = round(2.5 * fl / (res["attn_bwd_us"] * 1e-6) / 1e12, 1)
+        main = res["attn_bwd_us"] or res["attn_bwd_kv_us"]
+        res["bwd_kernel_tflops"] = round(2.5 * fl / (main * 1e-6) / 1e12, 1) if main else None
         res["bwd_total_tflops"] = round(2.5 * fl / (tot_bwd * 1e-6) / 1e12, 1)
         res["fwd_bwd_tflops"] = round(3.5 * fl / ((res["attn_fwd_us"] + tot_bwd) * 1e-6) / 1e12, 1)
         print(json.dumps(res), flush=True)

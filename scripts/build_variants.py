@@ -29,7 +29,7 @@ def main():
                 path = tok[5:]
             else:
                 extra.append(tok)
-        cmd = [B.HIPCC, *B.CFLAGS, *extra, f"-I{B.CSRC}", "-c", path, "-o", vobj]
+        cmd = [B.HIPCC, *B.CFLAGS, *B.FILE_FLAGS.get(src, []), *extra, f"-I{B.CSRC}", "-c", path, "-o", vobj]
         subprocess.run(cmd, check=True)
         lib = os.path.join(out_dir, f"{name}.so")
         link = [B.HIPCC, f"--offload-arch={B.ARCH}", "-shared", "-fPIC", "-o", lib,

@@ -66,21 +66,25 @@ def test_workspace_sizes(lib):
     assert lib.pico_rmsnorm_bwd_workspace_bytes(3, 2048) == 1 * 2048 * 4
     from picotron_amd import _lib
     a = _lib.AttnArgs()
-    a.batch, a.seqlen_q, a.seqlen_k, a.heads_q, a.head_dim = 4, 1024, 1024, 32, 64
-    # LSE*log2e + delta ([B*Hq][Sq padded to 32]) + one fp32 dQ partial slab per 256-key block
-    # (+ 64 floats of trash for padded-row dQ stores)
-    assert lib.pico_attn_bwd_workspace_bytes(ctypes.byref(a)) == 2 * 4 * 32 * 1024 * 4 + 4 * (4 * 1024 * 32 * 64 * 4) + 256
+    a.batch, a.seqlen_q, a.seqlen_k, a.heads_q, a.heads_kv, a.head_dim = 4, 1024, 1024, 32, 32, 64
+    # head_dim 64 (split backward): LSE*log2e + delta, each [B*Hq][Sq padded to 32] fp32 — nothing else
+    assert lib.pico_attn_bwd_workspace_bytes(ctypes.byref(a)) == 2 * 4 * 32 * 1024 * 4
     a.seqlen_q = a.seqlen_k = 1000
     pad = ((4 * 32 * 1024 + 63) // 64) * 64
-    assert lib.pico_attn_bwd_workspace_bytes(ctypes.byref(a)) == 2 * pad * 4 + 4 * (4 * 1000 * 32 * 64 * 4) + 256
-    # GQA 32/8 at S 1024: 4 key blocks x B 4 x 8 kv heads = 128 workgroups -> query heads split 4 ways,
-    # + fp32 dK/dV partials [4][2][B, S, Hkv, D]
+    assert lib.pico_attn_bwd_workspace_bytes(ctypes.byref(a)) == 2 * pad * 4
+    # GQA 32/8 at S 1024: 4 key blocks x B 4 x 8 kv heads = 128 workgroups -> tile lists split 2 ways,
+    # + fp32 dK/dV partials [2][2][B, S, Hkv, D]
     a.seqlen_q = a.seqlen_k = 1024
     a.heads_kv = 8
-    assert lib.pico_attn_bwd_workspace_bytes(ctypes.byref(a)) == (2 * 4 * 32 * 1024 * 4 + 4 * (4 * 1024 * 32 * 64 * 4)
-                                                                  + 256 + 4 * 2 * 4 * 1024 * 8 * 64 * 4)
-    a.heads_kv = 32  # MHA: no split
-    assert lib.pico_attn_bwd_workspace_bytes(ctypes.byref(a)) == 2 * 4 * 32 * 1024 * 4 + 4 * (4 * 1024 * 32 * 64 * 4) + 256
+    assert lib.pico_attn_bwd_workspace_bytes(ctypes.byref(a)) == 2 * 4 * 32 * 1024 * 4 + 2 * 2 * 4 * 1024 * 8 * 64 * 4
+    # O(S) at long sequences (the fused form's dQ slabs grew with S^2): 16K tokens, MHA
+    a.heads_kv = 32
+    a.batch, a.seqlen_q, a.seqlen_k = 1, 16384, 16384
+    assert lib.pico_attn_bwd_workspace_bytes(ctypes.byref(a)) == 2 * 32 * 16384 * 4
+    # head_dim 128 keeps the fused form: + one fp32 dQ partial slab per 256-key block (+ 64 trash floats)
+    a.batch, a.seqlen_q, a.seqlen_k, a.heads_q, a.heads_kv, a.head_dim = 2, 1024, 1024, 16, 16, 128
+    assert lib.pico_attn_bwd_workspace_bytes(ctypes.byref(a)) == 2 * 2 * 16 * 1024 * 4 + 4 * (2 * 1024 * 16 * 128 * 4) + 256 \
+        + 2 * 4 * 2 * 1024 * 16 * 128 * 4  # B 2 x 16 heads x 4 key blocks = 128 workgroups: dK/dV split 4 ways
 
 
 def test_ops_fail_loudly_without_hip_tensors(lib):

@@ -78,7 +78,10 @@ def _worker(rank, world, port, causal):
     n = S // world
     sl = slice(rank * n, (rank + 1) * n)
     ql, kl, vl = [t[:, sl].contiguous().requires_grad_(True) for t in (q, k, v)]
-    ol = CP.ring_attention(ql, kl, vl, scale, causal)
+    # exactly the reference's call (ref picotron/model.py:139-150): [B, S, H, D] projections transposed to
+    # [B, H, S, D], ring_attention, output transposed back to [B, S, H, D]
+    ol = CP.ring_attention(ql.transpose(1, 2), kl.transpose(1, 2), vl.transpose(1, 2), scale, causal).transpose(1, 2)
+    assert ol.shape == ql.shape
     ol.backward(do[:, sl].contiguous())
     torch.cuda.synchronize()
 
