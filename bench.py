@@ -101,7 +101,6 @@ def main():
                     help="process-group backend: nccl (= RCCL over xGMI, the product) or gloo (tests: several "
                          "ranks sharing one GPU, which RCCL refuses)")
     ap.add_argument("--no-kernel-timing", action="store_true")
-    ap.add_argument("--cpu-seq", type=int, default=256)
     ap.add_argument("--fused-adam", type=int, default=1,
                     help="AdamW(fused=True): the reference's use_fused_adam config (ref template/base_config.json:18, "
                          "train.py:204-207)")
@@ -117,6 +116,14 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+    # CPU baseline first, before this process touches the GPU (its gloo ranks are fresh processes):
+    # BASELINE.md's CPU plan, DP = 2 x 4 threads, SmolLM-1.7B geometry 2 layers, seq 1024 (oracle/cpu_baseline.py)
+    cpu_baseline = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle.cpu_baseline import dp2_cpu_throughput
+        t0 = time.time()
+        cpu_baseline = dp2_cpu_throughput()
+        log(f"[rank 0] cpu baseline {cpu_baseline['value']} tok/s ({time.time() - t0:.0f}s)")
     # one GPU per rank; ranks beyond the visible GPUs share them round-robin (gloo rehearsal only)
     device = torch.device("cuda", local_rank % torch.cuda.device_count())
     torch.cuda.set_device(device)
@@ -256,10 +263,6 @@ def main():
             v["total_ms"] = round(v["total_ms"], 3)
             v["avg_us"] = round(v["avg_us"], 2)
 
-    cpu_baseline = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu_baseline = run_cpu_baseline(cfg, model, args.cpu_seq)
-
     if rank == 0:
         out = {
             "metric": "tokens/sec/GPU + MFU, SmolLM-1.7B seq1024",
@@ -325,48 +328,6 @@ def measure_allreduce(model, world, device, reps=3):
     return {"buckets": len(bufs), "bytes": nbytes, "ms": round(1e3 * t, 3), "algbw_GBps": round(nbytes / t / 1e9, 1),
             "busbw_GBps": round(busbw, 1), "peak_GBps": peak, "frac": round(busbw / peak, 4),
             "single_link_GBps": XGMI_LINK_GBS, "timed_over": f"best of {reps} passes over all buckets, after the timed region"}
-
-
-def run_cpu_baseline(cfg, gpu_model, seq):
-    """Oracle (CPU restatement of the reference's eager fp32 path, oracle/model.py) timed on this
-    host's cores on a bounded sample of the same step: the full 15-layer SmolLM-1.7B, one micro-batch
-    of 1 x `seq` tokens, forward + backward + AdamW."""
-    from oracle import model as OM
-    ncores = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-    torch.set_num_threads(ncores)
-    from types import SimpleNamespace
-    ocfg = SimpleNamespace(**{**cfg.__dict__, "max_position_embeddings": seq})
-    with torch.device("meta"):
-        m = OM.Llama(ocfg)
-    m.to_empty(device="cpu")
-    from oracle import hotpath as H
-    D = cfg.hidden_size // cfg.num_attention_heads
-    for layer in m.decoder_layers:
-        layer.cos, layer.sin = H.get_cos_sin(seq, D, cfg.rope_theta)
-    src = dict(gpu_model.named_parameters())
-    with torch.no_grad():  # same weights as the GPU model (fp32), no CPU RNG init cost
-        for n, p in m.named_parameters():
-            key = n if n in src else "module." + n
-            p.copy_(src[key].detach().float().cpu())
-    opt = torch.optim.AdamW(m.parameters(), lr=3e-4)
-    gen = torch.Generator().manual_seed(0)
-    toks = torch.randint(0, cfg.vocab_size, (1, seq + 1), generator=gen)
-    batch = [(toks[:, :-1], toks[:, 1:])]
-    OM.train_step(m, batch, 1)  # warm-up (allocations)
-    opt.zero_grad()
-    t0 = time.perf_counter()
-    n = 0
-    while True:
-        OM.train_step(m, batch, 1)
-        opt.step()
-        opt.zero_grad()
-        n += 1
-        if time.perf_counter() - t0 > 10.0 or n >= 3:
-            break
-    dt = time.perf_counter() - t0
-    return {"value": round(n * seq / dt, 2), "unit": "tokens/s", "cores": ncores, "kind": "port",
-            "sample": f"{n} x full step (fwd+bwd+AdamW) of SmolLM-1.7B-15L fp32 eager (oracle/model.py), "
-                      f"micro-batch 1x{seq} tokens, {dt:.1f}s"}
 
 
 if __name__ == "__main__":

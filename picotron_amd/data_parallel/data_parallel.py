@@ -88,10 +88,13 @@ class DataParallelBucket(nn.Module):
         world = bucket_manager.process_group_size
 
         def param_hook(*unused):
-            if getattr(param, "_pico_fused_pending", False):
-                # the wgrad GEMM / embedding kernel accumulated into main_grad itself and already
-                # marked the param ready (ops.wgrad_accumulate); AccumulateGrad got no gradient
-                param._pico_fused_pending = False
+            # A producer that accumulated into main_grad itself (fused wgrad GEMM, RMSNorm dw, embedding
+            # backward: ops.wgrad_accumulate / _norm_grad_target) hands autograd no gradient and has already
+            # marked the param ready; AccumulateGrad then normally skips its post-accumulate hooks, and if it
+            # does call them there is nothing to add. No state is carried between micro-batches, so a param
+            # may switch between the fused and the hook path at any micro-batch (PICO_WGRAD_FUSION toggled,
+            # a non-contiguous main_grad, TP layers swapped in) without dropping a gradient.
+            if param.grad is None:
                 return
             if param.requires_grad:
                 sync = self.require_backward_grad_sync
@@ -111,7 +114,6 @@ class DataParallelBucket(nn.Module):
     def _make_ready_fn(self, param, bucket_manager):
         def ready():
             # the GEMM already did main_grad = (main_grad + dW) / W on the syncing micro-batch
-            param._pico_fused_pending = True
             if self.require_backward_grad_sync:
                 if not self._post_backward_callback_set:
                     Variable._execution_engine.queue_callback(self._post_backward)

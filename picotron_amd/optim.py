@@ -23,22 +23,23 @@ class AdamW(torch.optim.Optimizer):
         defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, amsgrad=False, maximize=False,
                         foreach=None, capturable=False, differentiable=False, fused=fused)
         super().__init__(params, defaults)
-        self._tables = {}  # group index -> (key, tensors_dev, sizes_dev, chunks_dev, n_chunks, pinned host table)
-        self._copy_done = None  # event after the last host -> device table copy
+        self._tables = {}  # (group index, step) -> [key, tensors_dev, sizes_dev, chunks_dev, n_chunks, pinned table, event]
 
-    def _group_tables(self, gi, params):
+    def _group_tables(self, gi, step, params):
         chunk = int(_lib.load().pico_adamw_chunk_elems())
         key = tuple((p.data_ptr(), p.numel()) for p in params)
-        ent = self._tables.get(gi)
+        ent = self._tables.get((gi, step))
         if ent is None or ent[0] != key:
             sizes = torch.tensor([p.numel() for p in params], dtype=torch.int64)
             chunks = [(i, c) for i, p in enumerate(params) for c in range(0, p.numel(), chunk)]
             dev = params[0].device
             chunks_t = torch.tensor(chunks, dtype=torch.int64).reshape(-1, 2)
             host = torch.empty((len(params), 4), dtype=torch.int64).pin_memory()
-            ent = (key, torch.empty((len(params), 4), dtype=torch.int64, device=dev), sizes.to(dev),
-                   chunks_t.to(dev), len(chunks), host)
-            self._tables[gi] = ent
+            ent = [key, torch.empty((len(params), 4), dtype=torch.int64, device=dev), sizes.to(dev),
+                   chunks_t.to(dev), len(chunks), host, None]
+            if len(self._tables) > 64:  # step counts keep changing (params joining late): keep the map small
+                self._tables.clear()
+            self._tables[(gi, step)] = ent
         return ent
 
     @torch.no_grad()
@@ -52,33 +53,41 @@ class AdamW(torch.optim.Optimizer):
             params = [p for p in group["params"] if p.grad is not None]
             if not params:
                 continue
-            steps = set()
+            # validate everything before touching any state (a failed step leaves the state as it was)
             for p in params:
                 if not (p.is_cuda and p.dtype == torch.bfloat16 and p.grad.dtype == torch.bfloat16):
                     raise TypeError("picotron_amd.optim.AdamW: parameters and gradients must be bf16 HIP tensors, "
                                     f"got {p.dtype} / {p.grad.dtype} on {p.device}")
                 if p.grad.is_sparse or not p.grad.is_contiguous() or not p.is_contiguous():
                     raise ValueError("picotron_amd.optim.AdamW: dense contiguous parameters and gradients only")
+            # per-parameter step counts, as torch.optim.AdamW keeps them: a parameter that had no gradient on
+            # some steps (frozen for a while, an idle pipeline stage) advances only when it has one; one
+            # launch per distinct step count. `step` stays a CPU scalar (a loaded state may carry it on the
+            # device: moved back once, so reading it costs no host sync per step).
+            by_step = {}
+            for p in params:
                 st = self.state[p]
                 if not st:
                     st["step"] = torch.tensor(0.0, dtype=torch.float32)
                     st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                     st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                elif st["step"].device.type != "cpu":
+                    st["step"] = st["step"].detach().to("cpu", torch.float32)
                 st["step"] += 1
-                steps.add(int(st["step"].item()))
-            if len(steps) != 1:
-                raise RuntimeError("picotron_amd.optim.AdamW: parameters of one group at different step counts")
-            key, tens, sizes, chunks, n_chunks, host = self._group_tables(gi, params)
-            if self._copy_done is not None:  # the pinned table may still be feeding the previous copy
-                self._copy_done.synchronize()
-            host.numpy()[:] = [(p.data_ptr(), p.grad.data_ptr(), self.state[p]["exp_avg"].data_ptr(),
-                                self.state[p]["exp_avg_sq"].data_ptr()) for p in params]
-            tens.copy_(host, non_blocking=True)
-            self._copy_done = torch.cuda.Event()
-            self._copy_done.record(torch.cuda.current_stream(params[0].device))
+                by_step.setdefault(int(st["step"].item()), []).append(p)
             beta1, beta2 = group["betas"]
-            _lib.check(lib.pico_adamw_bf16(_lib.ptr(tens), _lib.ptr(sizes), _lib.ptr(chunks), n_chunks,
-                                           float(group["lr"]), float(beta1), float(beta2), float(group["eps"]),
-                                           float(group["weight_decay"]), steps.pop(), _lib.stream_of(params[0])),
-                       "pico_adamw_bf16")
+            for step, ps in sorted(by_step.items()):
+                ent = self._group_tables(gi, step, ps)
+                _, tens, sizes, chunks, n_chunks, host, done = ent
+                if done is not None:  # the pinned table may still be feeding this entry's previous copy
+                    done.synchronize()
+                host.numpy()[:] = [(p.data_ptr(), p.grad.data_ptr(), self.state[p]["exp_avg"].data_ptr(),
+                                    self.state[p]["exp_avg_sq"].data_ptr()) for p in ps]
+                tens.copy_(host, non_blocking=True)
+                ent[6] = torch.cuda.Event()
+                ent[6].record(torch.cuda.current_stream(ps[0].device))
+                _lib.check(lib.pico_adamw_bf16(_lib.ptr(tens), _lib.ptr(sizes), _lib.ptr(chunks), n_chunks,
+                                               float(group["lr"]), float(beta1), float(beta2), float(group["eps"]),
+                                               float(group["weight_decay"]), step, _lib.stream_of(ps[0])),
+                           "pico_adamw_bf16")
         return loss

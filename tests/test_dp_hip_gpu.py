@@ -1,0 +1,113 @@
+"""DataParallelBucket on the HIP path at world size 2: two gloo
+ranks share one GPU and run the product model — fused LM-head CE, fused wgrad accumulation into the fp32
+main_grad with 1/W folded into the syncing GEMMs, RMSNorm dw mode 2, embedding backward into main_grad,
+the bucket all-reduce and the bf16 cast on the side stream — over grad_acc = 3 micro-batches
+(ref picotron/data_parallel/data_parallel.py:62-171, bucket.py:6-57; ref train.py:29-55 micro-batch loop).
+
+  * same data on both ranks: main_grad and .grad must equal, bit for bit, a one-rank run of the same
+    micro-batches (the average of two identical sums is the sum: /2 and x/2 + x/2 are exact in fp32);
+  * different data per rank: main_grad must equal (within fp32 summation order, rel-L2 2e-6) half the
+    gradient sum of a one-rank run over both ranks' micro-batches, and .grad its bf16 cast bit for bit;
+  * PICO_WGRAD_FUSION flipped between micro-batches (fused -> plain -> fused): no micro-batch may be
+    dropped (the sticky per-param flag of round 1 could drop one).
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+GRAD_ACC = 3
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _batches(seed, n):
+    g = torch.Generator().manual_seed(seed)
+    toks = torch.randint(0, 512, (n, 2, 65), generator=g)
+    return [(t[:, :-1].contiguous(), t[:, 1:].contiguous()) for t in toks]
+
+
+def _worker(rank, world, port, seeds, toggle, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from picotron_amd import process_group_manager as pgm
+    from picotron_amd.data_parallel.data_parallel import DataParallelBucket
+    from picotron_amd.model import LlamaConfig, build_llama
+    from picotron_amd.train import _micro_batch
+
+    pgm.setup_process_group_manager(tp_size=1, cp_size=1, pp_size=1, dp_size=world)
+    cfg = LlamaConfig(hidden_size=256, intermediate_size=512, num_attention_heads=4, num_key_value_heads=2,
+                      num_hidden_layers=2, vocab_size=512, max_position_embeddings=64)
+    torch.manual_seed(42)
+    model = build_llama(cfg, device="cuda:0")
+    with torch.no_grad():  # the reference init zeroes the LM head (no gradient below it at step 0)
+        g = torch.Generator().manual_seed(7)
+        model.final_proj.weight.copy_(torch.randn(model.final_proj.weight.shape, generator=g) * 0.02)
+    model = DataParallelBucket(model)
+    batches = [b for s in seeds[rank] for b in _batches(s, GRAD_ACC)]
+    n = len(batches)
+    for i, (x, y) in enumerate(batches):
+        if toggle:
+            os.environ["PICO_WGRAD_FUSION"] = "0" if i % 3 == 1 else "1"
+        model.require_backward_grad_sync = i == n - 1
+        _micro_batch(model, x.cuda(), y.cuda(), GRAD_ACC)
+    torch.cuda.synchronize()
+    res = {name: (p.main_grad.detach().cpu().clone(), p.grad.detach().cpu().clone())
+           for name, p in model.module.named_parameters()}
+    torch.save(res, os.path.join(out_dir, f"r{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _run(world, seeds, toggle, tmp_path):
+    d = tmp_path / f"w{world}_{'t' if toggle else 'f'}_{abs(hash(str(seeds))) % 1000}"
+    d.mkdir()
+    mp.start_processes(_worker, args=(world, _free_port(), seeds, toggle, str(d)), nprocs=world, join=True,
+                       start_method="spawn")
+    return [torch.load(d / f"r{r}.pt", weights_only=True) for r in range(world)]
+
+
+def test_dp_w2_same_data_bit_exact(tmp_path):
+    w2 = _run(2, [[11], [11]], False, tmp_path)
+    w1 = _run(1, [[11]], False, tmp_path)[0]
+    for r in range(2):
+        for name, (mg, g) in w2[r].items():
+            assert torch.equal(mg, w1[name][0]), name
+            assert torch.equal(g, w1[name][1]), name
+    nz = sum(int((mg != 0).any()) for mg, _ in w1.values())
+    assert nz == len(w1)  # every parameter got a gradient
+
+
+def test_dp_w2_rank_data_matches_single_process_sum(tmp_path):
+    w2 = _run(2, [[21], [22]], False, tmp_path)
+    w1 = _run(1, [[21, 22]], False, tmp_path)[0]  # both ranks' micro-batches in one process: the sum
+    for r in range(2):
+        for name, (mg, g) in w2[r].items():
+            ref = w1[name][0] / 2
+            err = float((mg - ref).norm() / ref.norm().clamp_min(1e-30))
+            assert err < 2e-6, (name, err)
+            assert torch.equal(g, mg.to(torch.bfloat16)), name  # .grad = the bf16 cast of the averaged main_grad
+    for name in w2[0]:  # the all-reduce leaves both replicas identical
+        assert torch.equal(w2[0][name][0], w2[1][name][0])
+
+
+def test_dp_w2_fusion_toggled_between_micro_batches(tmp_path):
+    fused = _run(2, [[31], [32]], False, tmp_path)
+    mixed = _run(2, [[31], [32]], True, tmp_path)
+    for name, (mg, _) in fused[0].items():
+        err = float((mixed[0][name][0] - mg).norm() / mg.norm().clamp_min(1e-30))
+        # the plain path rounds each micro-batch's dW to bf16 before the fp32 accumulate: ~1e-3; a dropped
+        # micro-batch would be ~0.3
+        assert err < 2e-2, (name, err)

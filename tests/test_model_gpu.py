@@ -88,6 +88,61 @@ def test_loss_curve_overlays_reference(golden_loss):
     assert sum(abs(a - b) for a, b in zip(losses, ref32)) / 200 <= 0.25
 
 
+class _CycledLoader:
+    """train_step's loader protocol (ref picotron/data.py MicroBatchDataLoader: `grad_acc_steps`, next()
+    -> dict) over the golden run's 16 cycled micro-batches."""
+
+    def __init__(self, batches, grad_acc):
+        self.batches, self.grad_acc_steps, self.k = batches, grad_acc, 0
+
+    def __next__(self):
+        t = self.batches[self.k % len(self.batches)]
+        self.k += 1
+        return {"input_ids": t[:, :-1], "target_ids": t[:, 1:]}
+
+
+def test_loss_curve_shipped_path_overlays_reference(golden_loss):
+    """The 200-step overlay through exactly what bench.py times: train.train_step with
+    the fused LM-head + cross-entropy (_micro_batch), every micro-batch replayed from one HIP graph
+    (MicroBatchGraph), picotron_amd.optim.AdamW (pico_adamw_bf16), zero_grad(set_to_none=False) — against
+    the reference's bf16 curve, with the bounds of test_loss_curve_overlays_reference."""
+    from picotron_amd.data import synth_tokens
+    from picotron_amd.model import build_llama
+    from picotron_amd.optim import AdamW
+    from picotron_amd.train import MicroBatchGraph, train_step
+    cfg = golden_loss["config"]
+    torch.manual_seed(golden_loss["seed"])
+    m = build_llama(_cfg(golden_loss), device="cuda", dtype=BF)
+    opt = AdamW(m.parameters(), lr=golden_loss["lr"])
+    gen = torch.Generator().manual_seed(1234)
+    mbs, seq, ga = golden_loss["mbs"], golden_loss["seq"], golden_loss["grad_acc"]
+    loader = _CycledLoader([synth_tokens(mbs, seq + 1, cfg["vocab_size"], gen, "arith").cuda() for _ in range(16)], ga)
+
+    def zero():
+        for p in m.parameters():
+            if p.grad is not None:
+                p.grad.zero_()
+    graphs = MicroBatchGraph(m, ga, zero)
+    losses = []
+    for _ in range(200):
+        opt.zero_grad(set_to_none=False)
+        losses.append(train_step(m, loader, "cuda", graphs=graphs))
+        opt.step()
+    ref = golden_loss["losses_bf16"]
+    out = os.environ.get("PICO_LOSS_OUT")
+    if out:
+        import json
+        with open(out.replace(".json", "_shipped.json"), "w") as f:
+            json.dump({"gpu_bf16_shipped_path": losses, "reference_cpu_bf16": ref}, f)
+    # step 0 = ln V up to the bf16 rounding of each micro-batch's loss (the fused CE returns the loss in the
+    # logits' dtype, as ATen's does: ln 512 / 2 lies in [2, 4), 1 bf16 ulp = 0.0156)
+    assert abs(losses[0] - math.log(cfg["vocab_size"])) <= 0.02
+    diffs = [abs(a - b) for a, b in zip(losses, ref)]
+    for i in range(10, 200):
+        assert diffs[i] <= 0.06 + 0.03 * ref[i], (i, losses[i], ref[i])
+    assert sum(diffs) / len(diffs) <= 0.02
+
+
 def test_dp_bucket_rccl_world1(golden_loss, monkeypatch):
     """DataParallelBucket over RCCL (W=1): after grad_acc=2, main_grad == the fp32 sum of the two
     micro-batch bf16 grads and .grad == its bf16 cast — the reference's semantics — bit for bit

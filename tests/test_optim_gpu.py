@@ -54,3 +54,48 @@ def test_adamw_rejects_non_bf16():
     p.grad = torch.randn(16, device="cuda")
     with pytest.raises(TypeError):
         AdamW([p]).step()
+
+
+def test_adamw_per_parameter_step_counts():
+    """A parameter without a gradient on some steps (frozen for a while, an idle pipeline stage) keeps its
+    own step count, as torch.optim.AdamW does: same result as torch's fused AdamW."""
+    from picotron_amd.optim import AdamW
+    torch.manual_seed(1)
+    base = [torch.randn(s, device="cuda").to(BF) for s in [(512,), (64, 32), (300,)]]
+    ours = [torch.nn.Parameter(t.clone()) for t in base]
+    ref = [torch.nn.Parameter(t.clone()) for t in base]
+    o1 = AdamW(ours, lr=1e-2, weight_decay=0.01)
+    o2 = torch.optim.AdamW(ref, lr=1e-2, weight_decay=0.01, fused=True)
+    for step in range(5):
+        for i, (a, b) in enumerate(zip(ours, ref)):
+            if i == 1 and step in (0, 2):  # parameter 1 idles on steps 0 and 2
+                a.grad = b.grad = None
+                continue
+            g = torch.randn(a.shape, device="cuda").to(BF)
+            a.grad = g.clone()
+            b.grad = g.clone()
+        o1.step()
+        o2.step()
+        for a, b in zip(ours, ref):
+            d = _ulp_diff(a.detach(), b.detach())
+            bad = (d > 1) & ((a.detach().float() - b.detach().float()).abs() > 1e-12)
+            assert not bool(bad.any()), (step, tuple(a.shape), int(d.max()))
+            with torch.no_grad():
+                a.copy_(b)
+                if b in o2.state:
+                    o1.state[a]["exp_avg"].copy_(o2.state[b]["exp_avg"])
+                    o1.state[a]["exp_avg_sq"].copy_(o2.state[b]["exp_avg_sq"])
+    assert [float(o1.state[p]["step"]) for p in ours] == [5.0, 3.0, 5.0]
+    assert [float(o2.state[p]["step"]) for p in ref] == [5.0, 3.0, 5.0]
+
+
+def test_adamw_bad_step_leaves_state_untouched():
+    from picotron_amd.optim import AdamW
+    p = torch.nn.Parameter(torch.randn(16, device="cuda").to(BF))
+    q = torch.nn.Parameter(torch.randn(16, device="cuda"))  # fp32: rejected
+    p.grad = torch.randn(16, device="cuda").to(BF)
+    q.grad = torch.randn(16, device="cuda")
+    opt = AdamW([p, q])
+    with pytest.raises(TypeError):
+        opt.step()
+    assert not opt.state[p]  # nothing was initialised or incremented
