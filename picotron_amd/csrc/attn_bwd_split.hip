@@ -32,7 +32,13 @@ namespace {
 
 constexpr int QB = 128;  // dq kernel: query rows per workgroup (4 waves x 32)
 constexpr int KT = 64;   // dq kernel: keys per tile
-constexpr int KVB = 256; // dkv kernel: keys per workgroup (4 waves x 64)
+constexpr int KVB = 256; // dkv kernel: keys per workgroup
+// dkv kernel: keys per wave. 64: 4 waves, one per SIMD, 2 key halves each (each Q/dO tile read serves 64
+// keys); 32: 8 waves, two per SIMD (the partner wave covers one wave's DMA issue and MFMA -> VALU waits)
+#ifndef PICO_KV_KPW
+#define PICO_KV_KPW 32
+#endif
+constexpr int KPW = PICO_KV_KPW, KH = KPW / 32, KNW = KVB / KPW;
 constexpr int QT = 32;   // dkv kernel: query rows per tile
 
 // PICO_BWDKV_STAMP: diagnostic build — workgroup 0 of the dK/dV kernel records s_memtime per (wave, tile,
@@ -41,7 +47,7 @@ constexpr int QT = 32;   // dkv kernel: query rows per tile
 #define PICO_BWDKV_STAMP 0
 #endif
 constexpr int STAMP_T = 48, STAMP_P = 5;
-constexpr int64_t STAMP_BYTES = PICO_BWDKV_STAMP ? 4 * STAMP_T * STAMP_P * 8 : 0;
+constexpr int64_t STAMP_BYTES = PICO_BWDKV_STAMP ? 8 * STAMP_T * STAMP_P * 8 : 0;
 
 #ifndef PICO_BWDQ_NBUF
 #define PICO_BWDQ_NBUF 3
@@ -68,7 +74,7 @@ struct KVCfg {
   static constexpr int RPP = 1024 / RB;
   static constexpr int NQP = QIMG / 1024;
   static constexpr int NP = 2 * NQP + 1;
-  static constexpr int NPW = (NP + 3) / 4;
+  static constexpr int NPW = (NP + KNW - 1) / KNW;
 };
 
 PICO_DEV float halves_sum2(float x) {
@@ -151,15 +157,19 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_q_kernel(const pico_attn_args
     dst_off[i] = (is_k[i] ? 0u : (unsigned)C::IMG) + (unsigned)jj * 1024u;
   }
   const unsigned smem_lds = (unsigned)__builtin_amdgcn_readfirstlane((int)lds_addr(smem));
+  unsigned full_off[C::NPW];  // per-lane byte offsets within a full tile (computed once)
+#pragma unroll
+  for (int i = 0; i < C::NPW; ++i) full_off[i] = (unsigned)(src_row[i] * (is_k[i] ? ksd : vsd) + src_col[i]) * 2u;
   auto issue = [&](int tile) __attribute__((always_inline)) {
     const unsigned slot = smem_lds + (unsigned)(tile % C::NBUF) * (unsigned)C::SLOT;
     const int base = tile * KT;
     const int lastrow = Sk - 1 - base;  // rows past it are clamped (finite; masked by the softmax)
+    const bool full = base + KT <= Sk;
 #pragma unroll
     for (int i = 0; i < C::NPW; ++i) {
-      const int row = min(src_row[i], lastrow);
       const void* tb = is_k[i] ? (const void*)(kg + (int64_t)base * ksd) : (const void*)(vg + (int64_t)base * vsd);
-      const unsigned off = (unsigned)(row * (is_k[i] ? ksd : vsd) + src_col[i]) * 2u;
+      const unsigned off = full ? full_off[i]
+                                : (unsigned)(min(src_row[i], lastrow) * (is_k[i] ? ksd : vsd) + src_col[i]) * 2u;
       dma_piece(tb, off, slot + dst_off[i]);
     }
   };
@@ -228,23 +238,29 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_q_kernel(const pico_attn_args
         kf[kt][ks] = lds_read_b128(kb, ro[ks] + kt * 32 * RB);
         vf[kt][ks] = lds_read_b128(vb, ro[ks] + kt * 32 * RB);
       }
+    // lane = query my_q; register i of half kt = key n0 + 32 kt + acc_row(i, h). The mask enters as the C
+    // operand of each S chain's first MFMA (as in attn_bwd_kv_kernel), keeping the tile one basic block.
     f32x16 s[2], dp[2];
+    if (mask) {  // wave-uniform: diagonal / partial tiles only
+      const int rel = lim_lane - n0 - 4 * h;  // key allowed iff (32 kt + (i&3) + 8 (i>>2)) <= rel
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        f32x16 m;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) m[i] = (32 * kt + (i & 3) + 8 * (i >> 2)) <= rel ? 0.f : -INFINITY;
+        s[kt] = mfma32(kf[kt][0], qf[0], m);
+      }
+    } else {
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) s[kt] = mfma32(kf[kt][0], qf[0], (f32x16)0.f);
+    }
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
-      s[kt] = mfma32(kf[kt][0], qf[0], (f32x16)0.f);
 #pragma unroll
       for (int ks = 1; ks < KS; ++ks) s[kt] = mfma32(kf[kt][ks], qf[ks], s[kt]);
       dp[kt] = mfma32(vf[kt][0], df[0], ndelta);
 #pragma unroll
       for (int ks = 1; ks < KS; ++ks) dp[kt] = mfma32(vf[kt][ks], df[ks], dp[kt]);
-    }
-    // lane = query my_q; register i of half kt = key n0 + 32 kt + acc_row(i, h)
-    if (mask) {  // wave-uniform: diagonal / partial tiles only
-      const int rel = lim_lane - n0 - 4 * h;  // key allowed iff (32 kt + (i&3) + 8 (i>>2)) <= rel
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) s[kt][i] = (32 * kt + (i & 3) + 8 * (i >> 2)) <= rel ? s[kt][i] : -INFINITY;
     }
     bf16x8 dsf[2][2];
 #pragma unroll
@@ -332,7 +348,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_q_kernel(const pico_attn_args
 // dK / dV kernel (key-major)
 // ------------------------------------------------------------------------------------------------
 template <int D, bool CAUSAL>
-__global__ __launch_bounds__(256, 1) void attn_bwd_kv_kernel(const pico_attn_args a, float scale, float scale_log2,
+__global__ __launch_bounds__(KNW * 64, KNW / 4) void attn_bwd_kv_kernel(const pico_attn_args a, float scale, float scale_log2,
                                                               const float* __restrict__ lse2_g,
                                                               const float* __restrict__ delta_g, int sq_pad,
                                                               int hsplit, float* __restrict__ dkv_part,
@@ -357,7 +373,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kv_kernel(const pico_attn_arg
   const int bh = bhs / hsplit;
   const int b = bh / (int)a.heads_kv, hk = bh % (int)a.heads_kv;
   const int k0 = kb * KVB;
-  const int kw = k0 + 64 * wave;  // this wave's first key
+  const int kw = k0 + KPW * wave;  // this wave's first key
 
   const int qstart = CAUSAL ? k0 : 0;  // k0 is a multiple of QT
   const int nqt = Sq > qstart ? (Sq - qstart + QT - 1) / QT : 0;
@@ -367,12 +383,12 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kv_kernel(const pico_attn_arg
   const int hq0 = hk * G + (nqt ? tb / nqt : 0), q00 = qstart + (nqt ? tb % nqt : 0) * QT;
 
   // ---- tile DMA: piece j issued by wave j % 4: Q pieces, dO pieces, then the LSE/delta piece ----
-  const int my_np = (C::NP / 4) + (wave < C::NP % 4 ? 1 : 0);
+  const int my_np = (C::NP / KNW) + (wave < C::NP % KNW ? 1 : 0);
   int pc_row[C::NPW], pc_col[C::NPW], pc_kind[C::NPW];
   unsigned pc_dst[C::NPW];
 #pragma unroll
   for (int i = 0; i < C::NPW; ++i) {
-    const int j = wave + 4 * i;
+    const int j = wave + KNW * i;
     if (j < 2 * C::NQP) {
       const int jj = j % C::NQP, row = C::RPP * jj + lane / CPR;
       pc_kind[i] = j < C::NQP ? 0 : 1;
@@ -402,28 +418,32 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kv_kernel(const pico_attn_arg
   const bf16_t* dobase = (const bf16_t*)a.dout + b * a.do_strides[0];
   const unsigned delta_off = (unsigned)((const char*)delta_g - (const char*)lse2_g);  // same workspace
   const unsigned ring_lds = (unsigned)__builtin_amdgcn_readfirstlane((int)lds_addr(smem));
+  // per-lane byte offsets of this wave's pieces within a full tile (computed once: the per-tile issue is
+  // then a scalar base + one DMA instruction per piece; partial tiles take the clamping path)
+  unsigned pc_off[C::NPW];
+#pragma unroll
+  for (int i = 0; i < C::NPW; ++i) {
+    if (pc_kind[i] == 2) pc_off[i] = (unsigned)pc_row[i] * 4u + (pc_col[i] ? delta_off : 0u);
+    else pc_off[i] = (unsigned)(pc_row[i] * (pc_kind[i] == 0 ? a.q_strides[1] : a.do_strides[1]) + pc_col[i]) * 2u;
+  }
   auto issue = [&](int si, Tc c) __attribute__((always_inline)) {
     const int hq = c.hq, q0 = c.q0;
     const bool full = q0 + QT <= Sq;
+    const unsigned dst = ring_lds + (unsigned)si * (unsigned)C::SLOT;
 #pragma unroll
     for (int i = 0; i < C::NPW; ++i) {
       if (i < my_np) {
         const void* base;
-        unsigned off;
+        unsigned off = pc_off[i];
         if (pc_kind[i] == 2) {
           base = lse2_g + ((int64_t)b * Hq + hq) * sq_pad + q0;
-          off = (unsigned)pc_row[i] * 4u + (pc_col[i] ? delta_off : 0u);
         } else {
-          const int dq = full ? pc_row[i] : min(q0 + pc_row[i], Sq - 1) - q0;
-          if (pc_kind[i] == 0) {
-            base = qbase + hq * a.q_strides[2] + (int64_t)q0 * a.q_strides[1];
-            off = (unsigned)(dq * a.q_strides[1] + pc_col[i]) * 2u;
-          } else {
-            base = dobase + hq * a.do_strides[2] + (int64_t)q0 * a.do_strides[1];
-            off = (unsigned)(dq * a.do_strides[1] + pc_col[i]) * 2u;
-          }
+          const int64_t s1 = pc_kind[i] == 0 ? a.q_strides[1] : a.do_strides[1];
+          base = pc_kind[i] == 0 ? (const void*)(qbase + hq * a.q_strides[2] + (int64_t)q0 * s1)
+                                 : (const void*)(dobase + hq * a.do_strides[2] + (int64_t)q0 * s1);
+          if (!full) off = (unsigned)((min(q0 + pc_row[i], Sq - 1) - q0) * s1 + pc_col[i]) * 2u;
         }
-        dma_piece(base, off, ring_lds + (unsigned)si * (unsigned)C::SLOT + pc_dst[i]);
+        dma_piece(base, off, dst + pc_dst[i]);
       }
     }
   };
@@ -438,9 +458,9 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kv_kernel(const pico_attn_arg
   // ---- K, V fragments of this wave's 64 keys (B operands of S = Q K^T, dP = dO V^T) ----
   const bf16_t* kg = (const bf16_t*)a.k + b * a.k_strides[0] + hk * a.k_strides[2];
   const bf16_t* vg = (const bf16_t*)a.v + b * a.v_strides[0] + hk * a.v_strides[2];
-  bf16x8 kf[2][KS], vf[2][KS];
+  bf16x8 kf[KH][KS], vf[KH][KS];
 #pragma unroll
-  for (int kt = 0; kt < 2; ++kt) {
+  for (int kt = 0; kt < KH; ++kt) {
     const int key = kw + 32 * kt + r;
     const bool ok = key < Sk;
     const bf16_t* kp = kg + (int64_t)min(key, Sk - 1) * a.k_strides[1] + 8 * h;
@@ -456,15 +476,15 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kv_kernel(const pico_attn_arg
 
   // consume the loads before the loop (see attn_bwd_q_kernel)
 #pragma unroll
-  for (int kt = 0; kt < 2; ++kt)
+  for (int kt = 0; kt < KH; ++kt)
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) asm volatile("" : "+a"(kf[kt][ks]), "+a"(vf[kt][ks]));
 
-  f32x16 dk[DT][2], dv[DT][2];
+  f32x16 dk[DT][KH], dv[DT][KH];
 #pragma unroll
   for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
+    for (int kt = 0; kt < KH; ++kt) {
       dk[dt][kt] = (f32x16)0.f;
       dv[dt][kt] = (f32x16)0.f;
     }
@@ -478,12 +498,12 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kv_kernel(const pico_attn_arg
 #pragma unroll
   for (int dt = 0; dt < DT; ++dt) asm volatile("" : "+v"(tro[dt][0]), "+v"(tro[dt][1]));
 
-  const bool kpad = kw + 63 >= Sk;  // wave-uniform: some of the wave's keys are padding
+  const bool kpad = kw + KPW - 1 >= Sk;  // wave-uniform: some of the wave's keys are padding
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();  // prologue tiles visible
 
 #if PICO_BWDKV_STAMP
-  __shared__ unsigned long long stamps[4 * STAMP_T * STAMP_P];
+  __shared__ unsigned long long stamps[KNW * STAMP_T * STAMP_P];
   auto stamp = [&](int t, int ph) __attribute__((always_inline)) {
     __builtin_amdgcn_sched_barrier(0);
     const unsigned long long v = __builtin_amdgcn_s_memtime();
@@ -493,6 +513,87 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kv_kernel(const pico_attn_arg
 #else
   auto stamp = [](int, int) __attribute__((always_inline)) {};
 #endif
+  // One 32-query tile in the order that lets one wave per SIMD overlap its own VALU with its MFMAs:
+  //   S, dP of key half 0 (8 MFMAs) | S, dP of half 1 (8) beside the softmax VALU of half 0 |
+  //   dV/dK of half 0 (8) beside the softmax VALU of half 1 | dV/dK of half 1 (8).
+  // A tile wholly above the wave's keys (causal) is masked to P = 0 rather than skipped: no per-wave branch
+  // around the body, and the slowest wave (wave 0) runs every tile anyway.
+  auto tile = [&](int si, int q0) __attribute__((always_inline)) {
+    const char* qs = smem + (unsigned)si * (unsigned)C::SLOT;
+    const char* dos = qs + C::QIMG;
+    const float* lsd = (const float*)(qs + 2 * C::QIMG);
+    bf16x8 qa[KS], da[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      qa[ks] = lds_read_b128(qs, qo[ks]);
+      da[ks] = lds_read_b128(dos, qo[ks]);
+    }
+    f32x16 nd;  // rows of this lane's accumulator registers: q = q0 + 8 g + 4 h + (0..3)
+    f32x4 l2[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(lsd + 32 + 8 * g + 4 * h);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) nd[4 * g + j] = v[j];
+      l2[g] = *reinterpret_cast<const f32x4*>(lsd + 8 * g + 4 * h);
+    }
+    // The causal / padding mask enters as the C operand of each S chain's first MFMA (-inf where key > q or
+    // key >= Sk, else 0): the branch covers only those two MFMAs, so the rest of the tile — S/dP chains,
+    // softmax VALU, dV/dK — is one basic block the scheduler can interleave.
+    f32x16 s[KH], dp[KH];
+    if ((CAUSAL && kw + KPW - 1 > q0) || kpad) {  // wave-uniform: diagonal / wholly masked tiles, padding keys
+#pragma unroll
+      for (int kt = 0; kt < KH; ++kt) {
+        const int key = kw + 32 * kt + r;
+        // masked iff (i&3) + 8(i>>2) < rel: causal key > q, or every row for a padding key
+        const int rel = key >= Sk ? 64 : (CAUSAL ? key - q0 - 4 * h : -1);
+        f32x16 m;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) m[i] = ((i & 3) + 8 * (i >> 2) < rel) ? -INFINITY : 0.f;
+        s[kt] = mfma32(qa[0], kf[kt][0], m);
+      }
+    } else {
+#pragma unroll
+      for (int kt = 0; kt < KH; ++kt) s[kt] = mfma32(qa[0], kf[kt][0], (f32x16)0.f);
+    }
+#pragma unroll
+    for (int kt = 0; kt < KH; ++kt) {
+#pragma unroll
+      for (int ks = 1; ks < KS; ++ks) s[kt] = mfma32(qa[ks], kf[kt][ks], s[kt]);
+      dp[kt] = mfma32(da[0], vf[kt][0], nd);
+#pragma unroll
+      for (int ks = 1; ks < KS; ++ks) dp[kt] = mfma32(da[ks], vf[kt][ks], dp[kt]);
+    }
+    bf16x8 dot[2][DT], qt[2][DT];
+#pragma unroll
+    for (int st = 0; st < 2; ++st)
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        dot[st][dt] = tr_pair(dos + 16 * st * RB, tro[dt][0], tro[dt][1]);
+        qt[st][dt] = tr_pair(qs + 16 * st * RB, tro[dt][0], tro[dt][1]);
+      }
+#pragma unroll
+    for (int kt = 0; kt < KH; ++kt) {
+      // P = exp2(S scale log2e - LSE log2e), dS = P dP'
+      float pv[16], sv[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        pv[i] = fast_exp2(__builtin_fmaf(s[kt][i], scale_log2, -l2[i >> 2][i & 3]));
+        sv[i] = pv[i] * dp[kt][i];
+      }
+      const bf16x8 pf[2] = {pack_bf16x8(pv), pack_bf16x8(pv + 8)};
+      const bf16x8 sf[2] = {pack_bf16x8(sv), pack_bf16x8(sv + 8)};
+      // dV^T[d][key] += dO^T[d][q] P[q][key],  dK^T[d][key] += Q^T[d][q] dS[q][key]
+#pragma unroll
+      for (int st = 0; st < 2; ++st)
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+          dv[dt][kt] = mfma32(dot[st][dt], pf[st], dv[dt][kt]);
+          dk[dt][kt] = mfma32(qt[st][dt], sf[st], dk[dt][kt]);
+        }
+    }
+  };
+
   Tc cur = {hq0, q00};
   int si = 0, si_nxt = PD % C::NBUF;
   for (int t = 0; t < ntiles; ++t) {
@@ -507,77 +608,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kv_kernel(const pico_attn_arg
     if (t + PD < ntiles) issue(si_nxt, nxt);
     advance(nxt);
     stamp(t, 2);
-    const int q0 = cur.q0;
-    // causal: the wave's keys all lie past the tile's last query row -> nothing to do
-    if (!CAUSAL || kw <= q0 + QT - 1) {
-      const char* qs = smem + (unsigned)si * (unsigned)C::SLOT;
-      const char* dos = qs + C::QIMG;
-      const float* lsd = (const float*)(qs + 2 * C::QIMG);
-      bf16x8 qa[KS], da[KS];
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        qa[ks] = lds_read_b128(qs, qo[ks]);
-        da[ks] = lds_read_b128(dos, qo[ks]);
-      }
-      // rows of this lane's accumulator registers: q = q0 + 8 g + 4 h + (0..3)
-      f32x4 l2[4];
-      f32x16 nd;
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        l2[g] = *reinterpret_cast<const f32x4*>(lsd + 8 * g + 4 * h);
-        const f32x4 v = *reinterpret_cast<const f32x4*>(lsd + 32 + 8 * g + 4 * h);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) nd[4 * g + j] = v[j];
-      }
-      f32x16 s[2], dp[2];
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt) {
-        s[kt] = mfma32(qa[0], kf[kt][0], (f32x16)0.f);
-#pragma unroll
-        for (int ks = 1; ks < KS; ++ks) s[kt] = mfma32(qa[ks], kf[kt][ks], s[kt]);
-        dp[kt] = mfma32(da[0], vf[kt][0], nd);
-#pragma unroll
-        for (int ks = 1; ks < KS; ++ks) dp[kt] = mfma32(da[ks], vf[kt][ks], dp[kt]);
-      }
-      stamp(t, 3);
-      if ((CAUSAL && kw + 63 > q0) || kpad) {  // wave-uniform: diagonal tiles / padding keys only
-#pragma unroll
-        for (int kt = 0; kt < 2; ++kt) {
-          const int key = kw + 32 * kt + r;
-          const int rel = CAUSAL ? key - q0 - 4 * h : -1;  // causal: masked iff (i&3) + 8(i>>2) < rel
-          const bool dead = key >= Sk;
-#pragma unroll
-          for (int i = 0; i < 16; ++i) s[kt][i] = (((i & 3) + 8 * (i >> 2) < rel) || dead) ? -INFINITY : s[kt][i];
-        }
-      }
-      bf16x8 pf[2][2], sf[2][2];
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt) {
-        float pv[16], sv[16];
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          pv[i] = fast_exp2(__builtin_fmaf(s[kt][i], scale_log2, -l2[i >> 2][i & 3]));
-          sv[i] = pv[i] * dp[kt][i];
-        }
-        pf[kt][0] = pack_bf16x8(pv);
-        pf[kt][1] = pack_bf16x8(pv + 8);
-        sf[kt][0] = pack_bf16x8(sv);
-        sf[kt][1] = pack_bf16x8(sv + 8);
-      }
-      // dV^T[d][key] += dO^T[d][q] P[q][key],  dK^T[d][key] += Q^T[d][q] dS[q][key]
-#pragma unroll
-      for (int st = 0; st < 2; ++st)
-#pragma unroll
-        for (int dt = 0; dt < DT; ++dt) {
-          const bf16x8 dot = tr_pair(dos + 16 * st * RB, tro[dt][0], tro[dt][1]);
-          const bf16x8 qt = tr_pair(qs + 16 * st * RB, tro[dt][0], tro[dt][1]);
-#pragma unroll
-          for (int kt = 0; kt < 2; ++kt) {
-            dv[dt][kt] = mfma32(dot, pf[kt][st], dv[dt][kt]);
-            dk[dt][kt] = mfma32(qt, sf[kt][st], dk[dt][kt]);
-          }
-        }
-    }
+    tile(si, cur.q0);
     stamp(t, 4);
     advance(cur);
     si = si + 1 == C::NBUF ? 0 : si + 1;
@@ -592,7 +623,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kv_kernel(const pico_attn_arg
   if (hsplit == 1) {
     const bool rope = (a.flags & PICO_ATTN_ROPE_BWD) != 0;
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
+    for (int kt = 0; kt < KH; ++kt) {
       const int key = kw + 32 * kt + r;
       if (key >= Sk) continue;
       if (rope) {
@@ -634,7 +665,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kv_kernel(const pico_attn_arg
     float* pk = dkv_part + (int64_t)(2 * hs) * part + ((int64_t)b * Sk * a.heads_kv + hk) * D;
     float* pv = pk + part;
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
+    for (int kt = 0; kt < KH; ++kt) {
       const int key = kw + 32 * kt + r;
       if (key >= Sk) continue;
 #pragma unroll
@@ -695,7 +726,7 @@ int launch_split(const pico_attn_args* a, hipStream_t s) {
   const int64_t nblk = (int64_t)nkb * a->batch * a->heads_kv * hsplit;
   if (nblk == 0) return 0;
   PICO_LAUNCH(PICO_K_ATTN_BWD_KV, "attn_bwd_kv", s,
-              attn_bwd_kv_kernel<D, CAUSAL><<<(int)nblk, 256, 0, s>>>(
+              attn_bwd_kv_kernel<D, CAUSAL><<<(int)nblk, KNW * 64, 0, s>>>(
                   *a, a->softmax_scale, sl2, lse2, delta, sq_pad, hsplit, dkv_part,
                   (unsigned long long*)((char*)a->workspace + pico_attn_bwd_split_workspace(a) - STAMP_BYTES)));
   if (hsplit > 1) {

@@ -36,8 +36,8 @@ def main():
     for _ in range(20):
         L.check(lib.pico_attn_bwd(ctypes.byref(a), L.stream_of(q)), "bwd")
     torch.cuda.synchronize()
-    off = nbytes - 4 * TILES * PH * 8
-    st = ws[off:].cpu().numpy().view(np.uint64).astype(np.int64).reshape(4, TILES, PH)
+    off = nbytes - 8 * TILES * PH * 8
+    st = ws[off:].cpu().numpy().view(np.uint64).astype(np.int64).reshape(-1, TILES, PH)
     ntiles = 32
     st = st[:, :ntiles]
     names = ["wait+barrier", "issue", "reads+S/dP", "softmax+dVdK", "loop"]
@@ -45,11 +45,11 @@ def main():
     for p in range(PH):
         nxt = st[:, :, p + 1] if p + 1 < PH else np.concatenate([st[:, 1:, 0], st[:, -1:, 0]], 1)
         d = (nxt - st[:, :, p])[:, 8: ntiles - 1]  # steady state: every wave active
-        out[names[p]] = [float(np.median(d[w])) for w in range(4)]
+        out[names[p]] = [float(np.median(d[w])) for w in range(st.shape[0])]
     tot = (st[:, -1, 0] - st[:, 0, 0]) / (ntiles - 1)
     out["per_tile_total"] = [float(x) for x in tot]
     print(json.dumps(out))
-    for w in range(4):
+    for w in range(st.shape[0]):
         print(w, (st[w, 16] - st[w, 16, 0]).tolist(), "next", int(st[w, 17, 0] - st[w, 16, 0]))
 
 
