@@ -68,6 +68,11 @@ def kernel_work(kid, cfg, mbs, seq):
     table = {
         L.K_ATTN_FWD: (attn_fwd, "flop", "mfma"),
         L.K_ATTN_BWD: (2.5 * attn_fwd, "flop", "mfma"),
+        # split backward (head_dim 64, csrc/attn_bwd_split.hip): EXECUTED products per kernel — the dQ kernel
+        # recomputes S and dP (3 products), the dK/dV kernel 4; the roofline entry for the backward prices
+        # the pair on the ALGORITHMIC 5 products (2.5 x forward) over the sum of the two launch times
+        L.K_ATTN_BWD_Q: (1.5 * attn_fwd, "flop", "mfma"),
+        L.K_ATTN_BWD_KV: (2.0 * attn_fwd, "flop", "mfma"),
         # residual-fused form (29 of 31 launches): fwd reads x, residual, writes y, residual_out and y^T
         # (the next projection's wgrad input); bwd reads dy, d(residual_out), x, writes dx (+4 B/row
         # rstd, small dw partials)
@@ -185,7 +190,8 @@ def main():
         loss = step()
         log(f"[rank {rank}] warmup {i}: loss {loss:.4f} ({time.time() - ts:.2f}s)")
 
-    kernel_ids = [L.K_ATTN_FWD, L.K_ATTN_BWD, L.K_ATTN_BWD_PRE, L.K_ATTN_BWD_DQ, L.K_RMSNORM_FWD, L.K_RMSNORM_BWD,
+    kernel_ids = [L.K_ATTN_FWD, L.K_ATTN_BWD, L.K_ATTN_BWD_Q, L.K_ATTN_BWD_KV, L.K_ATTN_BWD_PRE, L.K_ATTN_BWD_DQ,
+                  L.K_ATTN_BWD_DKV, L.K_RMSNORM_FWD, L.K_RMSNORM_BWD,
                   L.K_RMSNORM_DW, L.K_ROPE, L.K_SWIGLU_FWD, L.K_SWIGLU_BWD, L.K_GRAD_ACCUM, L.K_CAST]
     # Per-launch HIP events cannot ride inside a graph replay, so with graphs the kernels are timed
     # over one extra eagerly launched step right after the timed region (same shapes, same stream).
@@ -235,23 +241,6 @@ def main():
 
     roofline = None
     if kernels:
-        # dominant kernel = most total time among those with a stated algorithmic work
-        cand = [(v["total_ms"], name) for name, v in kernels.items()
-                if kernel_work([k for k in kernel_ids if L.KERNEL_NAMES[k] == name][0], cfg, MBS, SEQ)]
-        _, dom = max(cand)
-        kid = [k for k in kernel_ids if L.KERNEL_NAMES[k] == dom][0]
-        amount, unit, bound = kernel_work(kid, cfg, MBS, SEQ)
-        avg_s = kernels[dom]["avg_us"] * 1e-6
-        if unit == "flop":
-            achieved, peak, u = amount / avg_s / 1e12, BF16_PEAK_TFLOPS, "TFLOP/s"
-        else:
-            achieved, peak, u = amount / avg_s / 1e9, HBM_PEAK_GBS, "GB/s"
-        traffic, traffic_src = pmc_traffic(dom)
-        roofline = {"kernel": dom, "bound": bound, "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": u,
-                    "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_source": traffic_src,
-                    "work_per_launch": amount, "avg_launch_us": round(kernels[dom]["avg_us"], 2),
-                    "timed_over": ("the timed region" if kernel_timing_live else
-                                   "one eager step right after the timed region (graph replays carry no per-launch events)")}
         for name, v in kernels.items():
             kk = [k for k in kernel_ids if L.KERNEL_NAMES[k] == name][0]
             w = kernel_work(kk, cfg, MBS, SEQ)
@@ -260,6 +249,45 @@ def main():
                 v["achieved"] = round(a / 1e12, 2) if w[1] == "flop" else round(a / 1e9, 1)
                 v["unit"] = "TFLOP/s" if w[1] == "flop" else "GB/s"
                 v["frac"] = round(v["achieved"] / (BF16_PEAK_TFLOPS if w[1] == "flop" else HBM_PEAK_GBS), 4)
+        # candidates: (total ms, name, algorithmic work per launch, unit, bound, avg launch us, kernels)
+        cand = []
+        for name, v in kernels.items():
+            kk = [k for k in kernel_ids if L.KERNEL_NAMES[k] == name][0]
+            w = kernel_work(kk, cfg, MBS, SEQ)
+            if w and kk not in (L.K_ATTN_BWD_Q, L.K_ATTN_BWD_KV):
+                cand.append((v["total_ms"], name, w[0], w[1], w[2], v["avg_us"], [name]))
+        if "attn_bwd_q" in kernels and "attn_bwd_kv" in kernels:
+            # the split backward as ONE operation: 2.5 x forward FLOPs over the two kernels' mean launch times
+            q, kv = kernels["attn_bwd_q"], kernels["attn_bwd_kv"]
+            parts = ["attn_bwd_q", "attn_bwd_kv"] + (["attn_bwd_dkv"] if "attn_bwd_dkv" in kernels else [])
+            avg = sum(kernels[n]["avg_us"] * kernels[n]["launches"] / q["launches"] for n in parts)
+            cand.append((sum(kernels[n]["total_ms"] for n in parts), "attn_bwd_q+attn_bwd_kv",
+                         kernel_work(L.K_ATTN_BWD, cfg, MBS, SEQ)[0], "flop", "mfma", avg, parts))
+        _, dom, amount, unit, bound, avg_us, parts = max(cand)
+        avg_s = avg_us * 1e-6
+        if unit == "flop":
+            achieved, peak, u = amount / avg_s / 1e12, BF16_PEAK_TFLOPS, "TFLOP/s"
+        else:
+            achieved, peak, u = amount / avg_s / 1e9, HBM_PEAK_GBS, "GB/s"
+        traffic, srcs = 0, []
+        for n in parts:
+            t, src = pmc_traffic(n)
+            if t is None:
+                traffic = None
+                break
+            traffic += t
+            srcs.append(src)
+        roofline = {"kernel": dom, "bound": bound, "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": u,
+                    "frac": round(achieved / peak, 4), "traffic": traffic,
+                    "traffic_source": "; ".join(srcs) if traffic is not None else None,
+                    "work_per_launch": amount, "avg_launch_us": round(avg_us, 2),
+                    "timed_over": ("the timed region" if kernel_timing_live else
+                                   "one eager step right after the timed region (graph replays carry no per-launch events)")}
+        if len(parts) > 1:
+            roofline["note"] = ("algorithmic backward FLOPs (5 products, 2.5 x forward) over the summed mean launch "
+                                "times of " + " + ".join(parts) + "; the kernels execute 7 products (S and dP "
+                                "recomputed in the dQ kernel)")
+        for v in kernels.values():
             v["total_ms"] = round(v["total_ms"], 3)
             v["avg_us"] = round(v["avg_us"], 2)
 

@@ -28,11 +28,19 @@
 // one lane (accumulator tiles dt and dt + D/64), so it is register-local.
 #include "attn_common.h"
 
+
+
 namespace {
 
 constexpr int QB = 128;  // dq kernel: query rows per workgroup (4 waves x 32)
 constexpr int KT = 64;   // dq kernel: keys per tile
-constexpr int KVB = 256; // dkv kernel: keys per workgroup
+#ifndef PICO_KV_KVB
+#define PICO_KV_KVB 256
+#endif
+#ifndef PICO_KV_MINB
+#define PICO_KV_MINB 1
+#endif
+constexpr int KVB = PICO_KV_KVB;  // dkv kernel: keys per workgroup
 // dkv kernel: keys per wave. 64: 4 waves, one per SIMD, 2 key halves each (each Q/dO tile read serves 64
 // keys); 32: 8 waves, two per SIMD (the partner wave covers one wave's DMA issue and MFMA -> VALU waits)
 #ifndef PICO_KV_KPW
@@ -160,23 +168,29 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_q_kernel(const pico_attn_args
   unsigned full_off[C::NPW];  // per-lane byte offsets within a full tile (computed once)
 #pragma unroll
   for (int i = 0; i < C::NPW; ++i) full_off[i] = (unsigned)(src_row[i] * (is_k[i] ? ksd : vsd) + src_col[i]) * 2u;
-  auto issue = [&](int tile) __attribute__((always_inline)) {
-    const unsigned slot = smem_lds + (unsigned)(tile % C::NBUF) * (unsigned)C::SLOT;
+  // K and V tile rows advance by constant byte strides: wave-uniform pointers, bumped per tile
+  const int64_t kst = (int64_t)KT * ksd * 2, vst = (int64_t)KT * vsd * 2;
+  const char* kp_nxt = (const char*)kg;
+  const char* vp_nxt = (const char*)vg;
+  auto issue = [&](int tile, int slot_i) __attribute__((always_inline)) {
+    const unsigned slot = smem_lds + (unsigned)slot_i * (unsigned)C::SLOT;
     const int base = tile * KT;
     const int lastrow = Sk - 1 - base;  // rows past it are clamped (finite; masked by the softmax)
     const bool full = base + KT <= Sk;
 #pragma unroll
     for (int i = 0; i < C::NPW; ++i) {
-      const void* tb = is_k[i] ? (const void*)(kg + (int64_t)base * ksd) : (const void*)(vg + (int64_t)base * vsd);
+      const char* tb = is_k[i] ? kp_nxt : vp_nxt;
       const unsigned off = full ? full_off[i]
                                 : (unsigned)(min(src_row[i], lastrow) * (is_k[i] ? ksd : vsd) + src_col[i]) * 2u;
       dma_piece(tb, off, slot + dst_off[i]);
     }
+    kp_nxt += kst;
+    vp_nxt += vst;
   };
   constexpr int P = C::NBUF - 1;  // prefetch distance
 #pragma unroll
   for (int t = 0; t < P; ++t)
-    if (t < ntiles) issue(t);
+    if (t < ntiles) issue(t, t);
 
   // ---- Q, dO fragments (B operands), delta = rowsum(dO * O), LSE ----
   bf16x8 qf[KS], df[KS];
@@ -283,20 +297,26 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_q_kernel(const pico_attn_args
   };
 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // prologue tiles and loads landed
-  for (int t = 0; t < ntiles; ++t) {
-    if (t > 0) {  // tile t landed (this wave's pieces); the younger tiles stay in flight
-      if (P == 2 && t + 1 < ntiles) {
-        if constexpr (C::NPW == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // unrolled by the ring depth: every LDS read of a tile has a compile-time slot (immediate offsets)
+  for (int t0 = 0; t0 < ntiles; t0 += C::NBUF) {
+#pragma unroll
+    for (int u = 0; u < C::NBUF; ++u) {
+      const int t = t0 + u;
+      if (t >= ntiles) break;
+      if (t > 0) {  // tile t landed (this wave's pieces); the younger tiles stay in flight
+        if (P == 2 && t + 1 < ntiles) {
+          if constexpr (C::NPW == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+          else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        } else {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
       }
-    }
-    lds_barrier();  // every wave's pieces of tile t visible; slot (t + P) % NBUF no longer read
-    if (t + P < ntiles) issue(t + P);
-    const int n0 = t * KT;
-    if (n0 <= lim_last) {  // wave-uniform: some row of the wave sees some key of the tile
-      tile(smem + (unsigned)(t % C::NBUF) * (unsigned)C::SLOT, n0 + KT - 1 > lim_first, n0);
+      lds_barrier();  // every wave's pieces of tile t visible; slot (t + P) % NBUF no longer read
+      if (t + P < ntiles) issue(t + P, (u + P) % C::NBUF);
+      const int n0 = t * KT;
+      if (n0 <= lim_last) {  // wave-uniform: some row of the wave sees some key of the tile
+        tile(smem + u * C::SLOT, n0 + KT - 1 > lim_first, n0);
+      }
     }
   }
 
@@ -348,7 +368,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_q_kernel(const pico_attn_args
 // dK / dV kernel (key-major)
 // ------------------------------------------------------------------------------------------------
 template <int D, bool CAUSAL>
-__global__ __launch_bounds__(KNW * 64, KNW / 4) void attn_bwd_kv_kernel(const pico_attn_args a, float scale, float scale_log2,
+__global__ __launch_bounds__(KNW * 64, PICO_KV_MINB) void attn_bwd_kv_kernel(const pico_attn_args a, float scale, float scale_log2,
                                                               const float* __restrict__ lse2_g,
                                                               const float* __restrict__ delta_g, int sq_pad,
                                                               int hsplit, float* __restrict__ dkv_part,
@@ -382,13 +402,12 @@ __global__ __launch_bounds__(KNW * 64, KNW / 4) void attn_bwd_kv_kernel(const pi
   const int ntiles = (int)((int64_t)ntot * (hs + 1) / hsplit) - tb;
   const int hq0 = hk * G + (nqt ? tb / nqt : 0), q00 = qstart + (nqt ? tb % nqt : 0) * QT;
 
-  // ---- tile DMA: piece j issued by wave j % 4: Q pieces, dO pieces, then the LSE/delta piece ----
-  const int my_np = (C::NP / KNW) + (wave < C::NP % KNW ? 1 : 0);
+  // ---- tile DMA: piece j = wave + KNW i: Q pieces, dO pieces, then the LSE/delta piece ----
   int pc_row[C::NPW], pc_col[C::NPW], pc_kind[C::NPW];
   unsigned pc_dst[C::NPW];
 #pragma unroll
   for (int i = 0; i < C::NPW; ++i) {
-    const int j = wave + KNW * i;
+    const int j = wave + KNW * i;  // wave-uniform
     if (j < 2 * C::NQP) {
       const int jj = j % C::NQP, row = C::RPP * jj + lane / CPR;
       pc_kind[i] = j < C::NQP ? 0 : 1;
@@ -403,52 +422,64 @@ __global__ __launch_bounds__(KNW * 64, KNW / 4) void attn_bwd_kv_kernel(const pi
       pc_dst[i] = 2 * C::QIMG;
     }
   }
+  // A tile = (query head hq, 32 query rows from q0). Each of this wave's pieces reads from one wave-uniform
+  // source pointer (Q rows, dO rows or the lse2 row) advanced by a constant stride per tile: the per-tile
+  // issue is one DMA instruction per piece (no 64-bit index arithmetic and no source select in the loop).
+  const int64_t qs1 = a.q_strides[1] * 2, ds1 = a.do_strides[1] * 2;  // bytes per query row
+  const char* const qbase = (const char*)((const bf16_t*)a.q + b * a.q_strides[0]);
+  const char* const dobase = (const char*)((const bf16_t*)a.dout + b * a.do_strides[0]);
+  int64_t pc_step[C::NPW];  // bytes per tile of piece i's source
+#pragma unroll
+  for (int i = 0; i < C::NPW; ++i) pc_step[i] = pc_kind[i] == 0 ? QT * qs1 : (pc_kind[i] == 1 ? QT * ds1 : QT * 4);
   struct Tc {
     int hq, q0;
+    const char* p[C::NPW];
+  };
+  auto make_tc = [&](int hq, int q0) __attribute__((always_inline)) {
+    Tc c;
+    c.hq = hq;
+    c.q0 = q0;
+#pragma unroll
+    for (int i = 0; i < C::NPW; ++i)
+      c.p[i] = pc_kind[i] == 0 ? qbase + hq * a.q_strides[2] * 2 + q0 * qs1
+             : pc_kind[i] == 1 ? dobase + hq * a.do_strides[2] * 2 + q0 * ds1
+                               : (const char*)(lse2_g + ((int64_t)b * Hq + hq) * sq_pad + q0);
+    return c;
   };
   const int qend = qstart + nqt * QT;
   auto advance = [&](Tc& c) __attribute__((always_inline)) {
-    c.q0 += QT;
-    if (c.q0 >= qend) {
-      c.q0 = qstart;
-      ++c.hq;
+    if (c.q0 + QT >= qend) {
+      c = make_tc(c.hq + 1, qstart);
+    } else {
+      c.q0 += QT;
+#pragma unroll
+      for (int i = 0; i < C::NPW; ++i) c.p[i] += pc_step[i];
     }
   };
-  const bf16_t* qbase = (const bf16_t*)a.q + b * a.q_strides[0];
-  const bf16_t* dobase = (const bf16_t*)a.dout + b * a.do_strides[0];
   const unsigned delta_off = (unsigned)((const char*)delta_g - (const char*)lse2_g);  // same workspace
   const unsigned ring_lds = (unsigned)__builtin_amdgcn_readfirstlane((int)lds_addr(smem));
-  // per-lane byte offsets of this wave's pieces within a full tile (computed once: the per-tile issue is
-  // then a scalar base + one DMA instruction per piece; partial tiles take the clamping path)
+  // per-lane byte offsets of this wave's pieces within a full tile (computed once; partial tiles clamp)
   unsigned pc_off[C::NPW];
 #pragma unroll
   for (int i = 0; i < C::NPW; ++i) {
     if (pc_kind[i] == 2) pc_off[i] = (unsigned)pc_row[i] * 4u + (pc_col[i] ? delta_off : 0u);
-    else pc_off[i] = (unsigned)(pc_row[i] * (pc_kind[i] == 0 ? a.q_strides[1] : a.do_strides[1]) + pc_col[i]) * 2u;
+    else pc_off[i] = (unsigned)(pc_row[i] * (pc_kind[i] == 0 ? qs1 : ds1) + pc_col[i] * 2);
   }
-  auto issue = [&](int si, Tc c) __attribute__((always_inline)) {
-    const int hq = c.hq, q0 = c.q0;
-    const bool full = q0 + QT <= Sq;
+  const bool ragged = Sq % QT != 0;
+  auto issue = [&](int si, const Tc& c) __attribute__((always_inline)) {
     const unsigned dst = ring_lds + (unsigned)si * (unsigned)C::SLOT;
 #pragma unroll
     for (int i = 0; i < C::NPW; ++i) {
-      if (i < my_np) {
-        const void* base;
+      if (i < C::NP / KNW || wave < C::NP % KNW) {
         unsigned off = pc_off[i];
-        if (pc_kind[i] == 2) {
-          base = lse2_g + ((int64_t)b * Hq + hq) * sq_pad + q0;
-        } else {
-          const int64_t s1 = pc_kind[i] == 0 ? a.q_strides[1] : a.do_strides[1];
-          base = pc_kind[i] == 0 ? (const void*)(qbase + hq * a.q_strides[2] + (int64_t)q0 * s1)
-                                 : (const void*)(dobase + hq * a.do_strides[2] + (int64_t)q0 * s1);
-          if (!full) off = (unsigned)((min(q0 + pc_row[i], Sq - 1) - q0) * s1 + pc_col[i]) * 2u;
-        }
-        dma_piece(base, off, dst + pc_dst[i]);
+        if (ragged && c.q0 + QT > Sq && pc_kind[i] != 2)  // partial tile: clamp rows past Sq - 1
+          off = (unsigned)((min(c.q0 + pc_row[i], Sq - 1) - c.q0) * (pc_kind[i] == 0 ? qs1 : ds1) + pc_col[i] * 2);
+        dma_piece(c.p[i], off, dst + pc_dst[i]);
       }
     }
   };
   constexpr int PD = C::PD;
-  Tc nxt = {hq0, q00};
+  Tc nxt = make_tc(hq0, q00);
 #pragma unroll
   for (int j = 0; j < PD; ++j) {
     if (j < ntiles) issue(j, nxt);
@@ -478,7 +509,7 @@ __global__ __launch_bounds__(KNW * 64, KNW / 4) void attn_bwd_kv_kernel(const pi
 #pragma unroll
   for (int kt = 0; kt < KH; ++kt)
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) asm volatile("" : "+a"(kf[kt][ks]), "+a"(vf[kt][ks]));
+    for (int ks = 0; ks < KS; ++ks) asm volatile("" : "+v"(kf[kt][ks]), "+v"(vf[kt][ks]));
 
   f32x16 dk[DT][KH], dv[DT][KH];
 #pragma unroll
@@ -513,12 +544,11 @@ __global__ __launch_bounds__(KNW * 64, KNW / 4) void attn_bwd_kv_kernel(const pi
 #else
   auto stamp = [](int, int) __attribute__((always_inline)) {};
 #endif
-  // One 32-query tile in the order that lets one wave per SIMD overlap its own VALU with its MFMAs:
-  //   S, dP of key half 0 (8 MFMAs) | S, dP of half 1 (8) beside the softmax VALU of half 0 |
-  //   dV/dK of half 0 (8) beside the softmax VALU of half 1 | dV/dK of half 1 (8).
-  // A tile wholly above the wave's keys (causal) is masked to P = 0 rather than skipped: no per-wave branch
-  // around the body, and the slowest wave (wave 0) runs every tile anyway.
-  auto tile = [&](int si, int q0) __attribute__((always_inline)) {
+  // One 32-query tile = M1 (S = Q K^T and dP = dO V^T - delta: 8 MFMAs, mask and -delta in the C operand),
+  // then V (P = exp2(S scale log2e - LSE log2e), dS = P dP: VALU) and M2 (dV^T += dO^T P, dK^T += Q^T dS:
+  // 8 MFMAs with the packed accumulators as B operands). A tile wholly above the wave's keys (causal) is
+  // masked to P = 0 rather than skipped (no per-wave branch around the body).
+  auto m1 = [&](int si, int q0, f32x16 (&s)[KH], f32x16 (&dp)[KH]) __attribute__((always_inline)) {
     const char* qs = smem + (unsigned)si * (unsigned)C::SLOT;
     const char* dos = qs + C::QIMG;
     const float* lsd = (const float*)(qs + 2 * C::QIMG);
@@ -529,18 +559,14 @@ __global__ __launch_bounds__(KNW * 64, KNW / 4) void attn_bwd_kv_kernel(const pi
       da[ks] = lds_read_b128(dos, qo[ks]);
     }
     f32x16 nd;  // rows of this lane's accumulator registers: q = q0 + 8 g + 4 h + (0..3)
-    f32x4 l2[4];
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const f32x4 v = *reinterpret_cast<const f32x4*>(lsd + 32 + 8 * g + 4 * h);
 #pragma unroll
       for (int j = 0; j < 4; ++j) nd[4 * g + j] = v[j];
-      l2[g] = *reinterpret_cast<const f32x4*>(lsd + 8 * g + 4 * h);
     }
     // The causal / padding mask enters as the C operand of each S chain's first MFMA (-inf where key > q or
-    // key >= Sk, else 0): the branch covers only those two MFMAs, so the rest of the tile — S/dP chains,
-    // softmax VALU, dV/dK — is one basic block the scheduler can interleave.
-    f32x16 s[KH], dp[KH];
+    // key >= Sk, else 0): the branch covers only those MFMAs, the rest of the tile is straight-line code.
     if ((CAUSAL && kw + KPW - 1 > q0) || kpad) {  // wave-uniform: diagonal / wholly masked tiles, padding keys
 #pragma unroll
       for (int kt = 0; kt < KH; ++kt) {
@@ -564,55 +590,78 @@ __global__ __launch_bounds__(KNW * 64, KNW / 4) void attn_bwd_kv_kernel(const pi
 #pragma unroll
       for (int ks = 1; ks < KS; ++ks) dp[kt] = mfma32(da[ks], vf[kt][ks], dp[kt]);
     }
-    bf16x8 dot[2][DT], qt[2][DT];
+  };
+  // V: P = exp2(S scale log2e - LSE log2e), dS = P dP, packed to bf16 (the B operands of M2)
+  auto vsm = [&](int si, const f32x16 (&s)[KH], const f32x16 (&dp)[KH], bf16x8 (&pf)[KH][2], bf16x8 (&sf)[KH][2])
+      __attribute__((always_inline)) {
+    const float* lsd = (const float*)(smem + (unsigned)si * (unsigned)C::SLOT + 2 * C::QIMG);
+    f32x4 l2[4];
 #pragma unroll
-    for (int st = 0; st < 2; ++st)
-#pragma unroll
-      for (int dt = 0; dt < DT; ++dt) {
-        dot[st][dt] = tr_pair(dos + 16 * st * RB, tro[dt][0], tro[dt][1]);
-        qt[st][dt] = tr_pair(qs + 16 * st * RB, tro[dt][0], tro[dt][1]);
-      }
+    for (int g = 0; g < 4; ++g) l2[g] = *reinterpret_cast<const f32x4*>(lsd + 8 * g + 4 * h);
 #pragma unroll
     for (int kt = 0; kt < KH; ++kt) {
-      // P = exp2(S scale log2e - LSE log2e), dS = P dP'
       float pv[16], sv[16];
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         pv[i] = fast_exp2(__builtin_fmaf(s[kt][i], scale_log2, -l2[i >> 2][i & 3]));
         sv[i] = pv[i] * dp[kt][i];
       }
-      const bf16x8 pf[2] = {pack_bf16x8(pv), pack_bf16x8(pv + 8)};
-      const bf16x8 sf[2] = {pack_bf16x8(sv), pack_bf16x8(sv + 8)};
-      // dV^T[d][key] += dO^T[d][q] P[q][key],  dK^T[d][key] += Q^T[d][q] dS[q][key]
-#pragma unroll
-      for (int st = 0; st < 2; ++st)
-#pragma unroll
-        for (int dt = 0; dt < DT; ++dt) {
-          dv[dt][kt] = mfma32(dot[st][dt], pf[st], dv[dt][kt]);
-          dk[dt][kt] = mfma32(qt[st][dt], sf[st], dk[dt][kt]);
-        }
+      pf[kt][0] = pack_bf16x8(pv);
+      pf[kt][1] = pack_bf16x8(pv + 8);
+      sf[kt][0] = pack_bf16x8(sv);
+      sf[kt][1] = pack_bf16x8(sv + 8);
     }
   };
+  // M2: dV^T[d][key] += dO^T[d][q] P[q][key], dK^T[d][key] += Q^T[d][q] dS[q][key] (A = transposed reads)
+  auto m2 = [&](int si, const bf16x8 (&pf)[KH][2], const bf16x8 (&sf)[KH][2]) __attribute__((always_inline)) {
+    const char* qs = smem + (unsigned)si * (unsigned)C::SLOT;
+    const char* dos = qs + C::QIMG;
+#pragma unroll
+    for (int st = 0; st < 2; ++st)
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        const bf16x8 dot = tr_pair(dos + 16 * st * RB, tro[dt][0], tro[dt][1]);
+        const bf16x8 qt = tr_pair(qs + 16 * st * RB, tro[dt][0], tro[dt][1]);
+#pragma unroll
+        for (int kt = 0; kt < KH; ++kt) {
+          dv[dt][kt] = mfma32(dot, pf[kt][st], dv[dt][kt]);
+          dk[dt][kt] = mfma32(qt, sf[kt][st], dk[dt][kt]);
+        }
+      }
+  };
 
-  Tc cur = {hq0, q00};
-  int si = 0, si_nxt = PD % C::NBUF;
-  for (int t = 0; t < ntiles; ++t) {
-    stamp(t, 0);
-    if (t > 0) {
-      // this wave's pieces of tile t landed; tile t + 1's (issued one iteration later) may stay in flight
-      if (t + 1 < ntiles) wait_vmcnt(my_np);
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      lds_barrier();  // everyone's pieces of tile t visible; slot (t + PD) % NBUF no longer read
+  // Unrolled by the ring depth: the slot of every LDS read is a compile-time constant (immediate offsets).
+  // (Measured and dropped, C2 causal: a stagger of the two waves of each SIMD by one phase — +2 %; carrying
+  // S / dP of tile t + 1 across the barrier so M1(t + 1) overlaps V(t) inside the wave — +6 %.)
+  int q0cur = q00;
+  for (int t0 = 0; t0 < ntiles; t0 += C::NBUF) {
+#pragma unroll
+    for (int u = 0; u < C::NBUF; ++u) {
+      const int t = t0 + u;
+      if (t >= ntiles) break;
+      stamp(t, 0);
+      if (t > 0) {
+        // this wave's pieces of tile t landed; tile t + 1's (issued one iteration later) may stay in flight
+        if (t + 1 < ntiles) {
+          if (wave < C::NP % KNW) wait_vmcnt(C::NP / KNW + 1);  // constant after inlining: one branch
+          else wait_vmcnt(C::NP / KNW);
+        } else {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        lds_barrier();  // everyone's pieces of tile t visible; slot (t + PD) % NBUF no longer read
+      }
+      stamp(t, 1);
+      if (t + PD < ntiles) issue((u + PD) % C::NBUF, nxt);
+      advance(nxt);
+      stamp(t, 2);
+      f32x16 s[KH], dp[KH];
+      bf16x8 pf[KH][2], sf[KH][2];
+      m1(u, q0cur, s, dp);
+      vsm(u, s, dp, pf, sf);
+      m2(u, pf, sf);
+      stamp(t, 4);
+      q0cur = q0cur + QT >= qend ? qstart : q0cur + QT;
     }
-    stamp(t, 1);
-    if (t + PD < ntiles) issue(si_nxt, nxt);
-    advance(nxt);
-    stamp(t, 2);
-    tile(si, cur.q0);
-    stamp(t, 4);
-    advance(cur);
-    si = si + 1 == C::NBUF ? 0 : si + 1;
-    si_nxt = si_nxt + 1 == C::NBUF ? 0 : si_nxt + 1;
   }
 
 #if PICO_BWDKV_STAMP

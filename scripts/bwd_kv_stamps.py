@@ -40,17 +40,17 @@ def main():
     st = ws[off:].cpu().numpy().view(np.uint64).astype(np.int64).reshape(-1, TILES, PH)
     ntiles = 32
     st = st[:, :ntiles]
-    names = ["wait+barrier", "issue", "reads+S/dP", "softmax+dVdK", "loop"]
+    phases = [("wait+barrier", 0, 1), ("issue", 1, 2), ("tile", 2, 4), ("loop", 4, None)]
     out = {}
-    for p in range(PH):
-        nxt = st[:, :, p + 1] if p + 1 < PH else np.concatenate([st[:, 1:, 0], st[:, -1:, 0]], 1)
-        d = (nxt - st[:, :, p])[:, 8: ntiles - 1]  # steady state: every wave active
-        out[names[p]] = [float(np.median(d[w])) for w in range(st.shape[0])]
+    for name, p0, p1 in phases:
+        nxt = st[:, :, p1] if p1 is not None else np.concatenate([st[:, 1:, 0], st[:, -1:, 0]], 1)
+        d = (nxt - st[:, :, p0])[:, 8: ntiles - 1]  # steady state: every wave active
+        out[name] = [float(np.median(d[w])) for w in range(st.shape[0])]
     tot = (st[:, -1, 0] - st[:, 0, 0]) / (ntiles - 1)
     out["per_tile_total"] = [float(x) for x in tot]
     print(json.dumps(out))
     for w in range(st.shape[0]):
-        print(w, (st[w, 16] - st[w, 16, 0]).tolist(), "next", int(st[w, 17, 0] - st[w, 16, 0]))
+        print(w, (st[w, 16, [0, 1, 2, 4]] - st[w, 16, 0]).tolist(), "next", int(st[w, 17, 0] - st[w, 16, 0]))
 
 
 if __name__ == "__main__":
