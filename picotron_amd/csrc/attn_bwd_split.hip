@@ -28,17 +28,23 @@
 // one lane (accumulator tiles dt and dt + D/64), so it is register-local.
 #include "attn_common.h"
 
+#include <type_traits>
+
 
 
 namespace {
 
 constexpr int QB = 128;  // dq kernel: query rows per workgroup (4 waves x 32)
 constexpr int KT = 64;   // dq kernel: keys per tile
+// dkv kernel workgroup: 128 keys = 4 waves (one per SIMD) of 32 keys, two workgroups resident per CU
+// (PICO_KV_MINB): independent workgroups overlap one's prologue (K/V fragments, first tiles) and epilogue
+// (dK/dV stores) with the other's main loop, which the 8-wave 256-key form (one workgroup per CU) could
+// not: C2 causal 62 vs 68 us.
 #ifndef PICO_KV_KVB
-#define PICO_KV_KVB 256
+#define PICO_KV_KVB 128
 #endif
 #ifndef PICO_KV_MINB
-#define PICO_KV_MINB 1
+#define PICO_KV_MINB 2
 #endif
 constexpr int KVB = PICO_KV_KVB;  // dkv kernel: keys per workgroup
 // dkv kernel: keys per wave. 64: 4 waves, one per SIMD, 2 key halves each (each Q/dO tile read serves 64
@@ -48,6 +54,9 @@ constexpr int KVB = PICO_KV_KVB;  // dkv kernel: keys per workgroup
 #endif
 constexpr int KPW = PICO_KV_KPW, KH = KPW / 32, KNW = KVB / KPW;
 constexpr int QT = 32;   // dkv kernel: query rows per tile
+#ifndef PICO_KV_PIPE
+#define PICO_KV_PIPE 0
+#endif
 
 // PICO_BWDKV_STAMP: diagnostic build — workgroup 0 of the dK/dV kernel records s_memtime per (wave, tile,
 // phase) and writes them after the workspace (pico_attn_bwd_split_workspace grows by STAMP_BYTES)
@@ -78,7 +87,9 @@ struct KVCfg {
   static constexpr int QIMG = QT * RB;   // one Q (or dO) tile image
   static constexpr int LSD = 1024;       // LSE*log2e [32] | -delta [32] (one DMA piece)
   static constexpr int SLOT = 2 * QIMG + LSD;
-  static constexpr int NBUF = 3, PD = 2;  // ring slots, prefetch distance
+  // PICO_KV_PIPE: the interval of tile t also reads slot t + 1 (S / dP of the next tile), so one more slot
+  static constexpr int PD = PICO_KV_PIPE ? 3 : 2;  // prefetch distance
+  static constexpr int NBUF = PD + 1;              // ring slots
   static constexpr int RPP = 1024 / RB;
   static constexpr int NQP = QIMG / 1024;
   static constexpr int NP = 2 * NQP + 1;
@@ -321,10 +332,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_q_kernel(const pico_attn_args
   }
 
   // ---- epilogue: lane = query my_q, register i of tile dt = d 32 dt + acc_row(i, h) ----
-  if (!row_ok) return;
+  // (every lane stays: the bf16 store's lane exchange needs the whole wave; only row_ok lanes store)
   if (a.flags & PICO_ATTN_ROPE_BWD) {  // rotate back by -theta: pairs (d, d + D/2) = tiles (dt, dt + DT/2)
-    const bf16_t* cp = (const bf16_t*)a.rope_cos + (int64_t)my_q * a.rope_stride;
-    const bf16_t* sp = (const bf16_t*)a.rope_sin + (int64_t)my_q * a.rope_stride;
+    const bf16_t* cp = (const bf16_t*)a.rope_cos + (int64_t)qc * a.rope_stride;
+    const bf16_t* sp = (const bf16_t*)a.rope_sin + (int64_t)qc * a.rope_stride;
 #pragma unroll
     for (int dt = 0; dt < DT / 2; ++dt)
 #pragma unroll
@@ -341,6 +352,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_q_kernel(const pico_attn_args
       }
   }
   if (a.flags & PICO_ATTN_DQ_F32_ACCUM) {
+    if (!row_ok) return;
     float* dst = (float*)a.dq + b * a.dq_strides[0] + hq * a.dq_strides[2] + (int64_t)my_q * a.dq_strides[1];
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt)
@@ -352,16 +364,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_q_kernel(const pico_attn_args
       }
     return;
   }
-  bf16_t* dst = (bf16_t*)a.dq + b * a.dq_strides[0] + hq * a.dq_strides[2] + (int64_t)my_q * a.dq_strides[1];
-#pragma unroll
-  for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      u16x4 w;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) w[j] = f2bf(dq[dt][4 * g + j] * scale);
-      *reinterpret_cast<u16x4*>(dst + 32 * dt + 8 * g + 4 * h) = w;
-    }
+  bf16_t* dst = (bf16_t*)a.dq + b * a.dq_strides[0] + hq * a.dq_strides[2] + (int64_t)qc * a.dq_strides[1];
+  store_row_bf16_x16<DT>(dst, h, row_ok, [&](int dt, int i) { return dq[dt][i] * scale; });
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -630,6 +634,113 @@ __global__ __launch_bounds__(KNW * 64, PICO_KV_MINB) void attn_bwd_kv_kernel(con
       }
   };
 
+#if PICO_KV_PIPE
+  // Software pipeline across tiles inside each wave: the interval of tile t (between two barriers) holds
+  // M1 of tile t + 1 and V + M2 of tile t, independent work in one basic block; sched_group_barrier
+  // spreads the softmax VALU of tile t between the S / dP MFMAs of tile t + 1. S / dP of the next tile
+  // are carried across the barrier in two alternating register sets (4-slot ring, unrolled by 4).
+  int q0cur = q00;
+  auto step = [&](auto uc, int t0, f32x16 (&sc)[KH], f32x16 (&dpc)[KH], f32x16 (&sn)[KH], f32x16 (&dpn)[KH])
+      __attribute__((always_inline)) -> bool {
+    constexpr int u = decltype(uc)::value;
+    const int t = t0 + u;
+    if (t >= ntiles) return false;
+    const int q0n = q0cur + QT >= qend ? qstart : q0cur + QT;
+    if (t + 1 < ntiles) {
+      // this wave's pieces of tile t + 1 landed (tile t + 2's may stay in flight)
+      if (t + 2 < ntiles) {
+        if (wave < C::NP % KNW) wait_vmcnt(C::NP / KNW + 1);
+        else wait_vmcnt(C::NP / KNW);
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      lds_barrier();  // everyone's pieces of tile t + 1 visible; slot (t + 3) % NBUF (tile t - 1) unread
+    }
+    if (t + PD < ntiles) issue((u + PD) % C::NBUF, nxt);
+    advance(nxt);
+    // S / dP of tile t + 1 (after the last tile: of a stale slot, discarded — keeps the body branch-free)
+    // interleaved by hand with V of tile t: fenced slices of {one M1 MFMA, two softmax elements}
+    static_assert(KH == 1, "the hand-interleaved body is written for 32 keys per wave");
+    constexpr int sn_slot = (u + 1) % C::NBUF;
+    const char* qs = smem + sn_slot * C::SLOT;
+    const char* cs = smem + u * C::SLOT;  // tile t
+    const float* lsd_c = (const float*)(cs + 2 * C::QIMG);
+    const float* lsd_n = (const float*)(qs + 2 * C::QIMG);
+    f32x4 l2[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) l2[g] = *reinterpret_cast<const f32x4*>(lsd_c + 8 * g + 4 * h);
+    bf16x8 qa[KS], da[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      qa[ks] = lds_read_b128(qs, qo[ks]);
+      da[ks] = lds_read_b128(qs + C::QIMG, qo[ks]);
+    }
+    f32x16 nd;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(lsd_n + 32 + 8 * g + 4 * h);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) nd[4 * g + j] = v[j];
+    }
+    if ((CAUSAL && kw + KPW - 1 > q0n) || kpad) {
+      const int key = kw + r;
+      const int rel = key >= Sk ? 64 : (CAUSAL ? key - q0n - 4 * h : -1);
+      f32x16 m;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) m[i] = ((i & 3) + 8 * (i >> 2) < rel) ? -INFINITY : 0.f;
+      sn[0] = mfma32(qa[0], kf[0][0], m);
+    } else {
+      sn[0] = mfma32(qa[0], kf[0][0], (f32x16)0.f);
+    }
+    float pv[16], sv[16];
+    bf16x8 pf[2], sf[2];
+    auto velem = [&](int i) __attribute__((always_inline)) {
+      pv[i] = fast_exp2(__builtin_fmaf(sc[0][i], scale_log2, -l2[i >> 2][i & 3]));
+      sv[i] = pv[i] * dpc[0][i];
+    };
+    bf16x8 dot[2][DT], qt[2][DT];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      __builtin_amdgcn_sched_barrier(0);
+      // M1 MFMAs 2..8 in slices 0..6: S ks = 1..KS-1, then the dP chain ks = 0..KS-1 (slice 7: none)
+      if (i < KS - 1) sn[0] = mfma32(qa[i + 1], kf[0][i + 1], sn[0]);
+      else if (i == KS - 1) dpn[0] = mfma32(da[0], vf[0][0], nd);
+      else if (i < 2 * KS - 1) dpn[0] = mfma32(da[i - KS + 1], vf[0][i - KS + 1], dpn[0]);
+      velem(2 * i);
+      velem(2 * i + 1);
+      if (i == 3) {
+        pf[0] = pack_bf16x8(pv);
+        sf[0] = pack_bf16x8(sv);
+      }
+      if (i >= 4) {  // M2's transposed operands, one (st, dt) pair per slice
+        const int st = (i - 4) >> 1, dt = (i - 4) & 1;
+        dot[st][dt] = tr_pair(cs + C::QIMG + 16 * st * RB, tro[dt][0], tro[dt][1]);
+        qt[st][dt] = tr_pair(cs + 16 * st * RB, tro[dt][0], tro[dt][1]);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    pf[1] = pack_bf16x8(pv + 8);
+    sf[1] = pack_bf16x8(sv + 8);
+#pragma unroll
+    for (int st = 0; st < 2; ++st)
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        dv[dt][0] = mfma32(dot[st][dt], pf[st], dv[dt][0]);
+        dk[dt][0] = mfma32(qt[st][dt], sf[st], dk[dt][0]);
+      }
+    q0cur = q0n;
+    return true;
+  };
+  f32x16 sA[KH], dA[KH], sB[KH], dB[KH];  // S / dP register sets: even tiles in A, odd tiles in B
+  if (ntiles > 0) m1(0, q00, sA, dA);
+  for (int t0 = 0; t0 < ntiles; t0 += C::NBUF) {
+    static_assert(C::NBUF == 4, "the unrolled body below assumes a 4-slot ring");
+    if (!step(std::integral_constant<int, 0>{}, t0, sA, dA, sB, dB)) break;
+    if (!step(std::integral_constant<int, 1>{}, t0, sB, dB, sA, dA)) break;
+    if (!step(std::integral_constant<int, 2>{}, t0, sA, dA, sB, dB)) break;
+    if (!step(std::integral_constant<int, 3>{}, t0, sB, dB, sA, dA)) break;
+  }
+#else
   // Unrolled by the ring depth: the slot of every LDS read is a compile-time constant (immediate offsets).
   // (Measured and dropped, C2 causal: a stagger of the two waves of each SIMD by one phase — +2 %; carrying
   // S / dP of tile t + 1 across the barrier so M1(t + 1) overlaps V(t) inside the wave — +6 %.)
@@ -664,6 +775,7 @@ __global__ __launch_bounds__(KNW * 64, PICO_KV_MINB) void attn_bwd_kv_kernel(con
     }
   }
 
+#endif
 #if PICO_BWDKV_STAMP
   if (blockIdx.x == 0)
     for (int i = lane; i < STAMP_T * STAMP_P; i += 64) stamp_out[wave * STAMP_T * STAMP_P + i] = stamps[wave * STAMP_T * STAMP_P + i];
@@ -674,10 +786,10 @@ __global__ __launch_bounds__(KNW * 64, PICO_KV_MINB) void attn_bwd_kv_kernel(con
 #pragma unroll
     for (int kt = 0; kt < KH; ++kt) {
       const int key = kw + 32 * kt + r;
-      if (key >= Sk) continue;
+      const int kc = min(key, Sk - 1);  // every lane runs the stores' lane exchange; only key < Sk store
       if (rope) {
-        const bf16_t* cp = (const bf16_t*)a.rope_cos + (int64_t)key * a.rope_stride;
-        const bf16_t* sp = (const bf16_t*)a.rope_sin + (int64_t)key * a.rope_stride;
+        const bf16_t* cp = (const bf16_t*)a.rope_cos + (int64_t)kc * a.rope_stride;
+        const bf16_t* sp = (const bf16_t*)a.rope_sin + (int64_t)kc * a.rope_stride;
 #pragma unroll
         for (int dt = 0; dt < DT / 2; ++dt)
 #pragma unroll
@@ -693,21 +805,10 @@ __global__ __launch_bounds__(KNW * 64, PICO_KV_MINB) void attn_bwd_kv_kernel(con
             }
           }
       }
-      bf16_t* dkp = (bf16_t*)a.dk + b * a.dk_strides[0] + hk * a.dk_strides[2] + (int64_t)key * a.dk_strides[1];
-      bf16_t* dvp = (bf16_t*)a.dv + b * a.dv_strides[0] + hk * a.dv_strides[2] + (int64_t)key * a.dv_strides[1];
-#pragma unroll
-      for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          u16x4 wk, wv;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            wk[j] = f2bf(dk[dt][kt][4 * g + j] * scale);
-            wv[j] = f2bf(dv[dt][kt][4 * g + j]);
-          }
-          *reinterpret_cast<u16x4*>(dkp + 32 * dt + 8 * g + 4 * h) = wk;
-          *reinterpret_cast<u16x4*>(dvp + 32 * dt + 8 * g + 4 * h) = wv;
-        }
+      bf16_t* dkp = (bf16_t*)a.dk + b * a.dk_strides[0] + hk * a.dk_strides[2] + (int64_t)kc * a.dk_strides[1];
+      bf16_t* dvp = (bf16_t*)a.dv + b * a.dv_strides[0] + hk * a.dv_strides[2] + (int64_t)kc * a.dv_strides[1];
+      store_row_bf16_x16<DT>(dkp, h, key < Sk, [&](int dt, int i) { return dk[dt][kt][i] * scale; });
+      store_row_bf16_x16<DT>(dvp, h, key < Sk, [&](int dt, int i) { return dv[dt][kt][i]; });
     }
   } else {  // fp32 partials [hs][dK | dV][b][key][hk][D]
     const int64_t part = a.batch * a.seqlen_k * a.heads_kv * D;
@@ -742,14 +843,14 @@ int64_t split_lsd_floats(const pico_attn_args* a) {
   return ((n + 63) / 64) * 64;
 }
 
-// split of a key block's tile list so that the dK/dV grid covers the 256 CUs (one workgroup each)
+// split of a key block's tile list so that the dK/dV grid fills the 256 CUs (PICO_KV_MINB workgroups each)
 int kv_hsplit(const pico_attn_args* a) {
   if (a->heads_kv <= 0 || a->heads_q % a->heads_kv != 0) return 1;
   const int64_t nblk = ((a->seqlen_k + KVB - 1) / KVB) * a->batch * a->heads_kv;
   const int64_t tiles = (a->heads_q / a->heads_kv) * ((a->seqlen_q + QT - 1) / QT);
   if (nblk <= 0) return 1;
   int d = 1;
-  while (d < 8 && nblk * d < 256 && 2 * d <= tiles) d *= 2;
+  while (d < 8 && nblk * d < 256 * PICO_KV_MINB && 2 * d <= tiles) d *= 2;
   return d;
 }
 

@@ -186,6 +186,37 @@ PICO_DEV void wait_vmcnt(int n) {
   }
 }
 
+// Stores one lane's 32x32 accumulator column(s) as a bf16 row with 16-byte stores: lane (r, h) holds
+// d = 32 dt + 8 g + 4 h + j (j < 4) of row r, so lanes l and l + 32 (the same row) exchange half-chunks
+// with v_permlane32_swap until each holds 8 consecutive d: lane h = 0 the even g, lane h = 1 the odd g
+// (half the store instructions of the 8-byte form; cdna_hip_programming.md T21). Every lane of the wave
+// must execute it (permlane: EXEC all ones); `ok` predicates only the stores.
+template <int DT, typename Get>
+PICO_DEV void store_row_bf16_x16(bf16_t* row, int h, bool ok, Get get) {
+  typedef __attribute__((ext_vector_type(2))) unsigned u32x2;
+  typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      u16x4 e, o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        e[j] = f2bf(get(dt, 4 * (2 * p) + j));
+        o[j] = f2bf(get(dt, 4 * (2 * p + 1) + j));
+      }
+      u32x2 ev = __builtin_bit_cast(u32x2, e), ov = __builtin_bit_cast(u32x2, o);
+#pragma unroll
+      for (int w = 0; w < 2; ++w) {
+        const auto rr = __builtin_amdgcn_permlane32_swap(ev[w], ov[w], false, false);
+        ev[w] = rr[0];
+        ov[w] = rr[1];
+      }
+      const u32x4 out = {ev[0], ev[1], ov[0], ov[1]};
+      if (ok) *reinterpret_cast<u32x4*>(row + 32 * dt + 8 * (2 * p + h)) = out;
+    }
+}
+
 // XOR applied to the 16-B chunk index of image row `row` (see lds_off in attn_common.h)
 template <int D>
 PICO_DEV int swz(int row) {
