@@ -120,7 +120,7 @@ class Bucket:
 
     def mark_param_as_ready(self, param: torch.nn.Parameter, prescaled: bool = False) -> None:
         assert param in self.params and param not in self.params_with_grad_ready, \
-            f"param {tuple(param.shape)} marked ready twice (or foreign)"
+            f"param {getattr(param, '_pico_name', '')}{tuple(param.shape)} marked ready twice (or foreign)"
         self.params_with_grad_ready.add(param)
         if prescaled:
             self.n_prescaled += 1

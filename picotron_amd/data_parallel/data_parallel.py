@@ -64,6 +64,8 @@ class DataParallelBucket(nn.Module):
         bucket_size = bucket_cap_mb * 1024 * 1024 // grad_size
         self.bucket_manager = BucketManager(module.parameters(), pgm.process_group_manager.cp_dp_group, bucket_size,
                                             grad_type)
+        self._fused_pass = set()  # params a fused producer accumulated in the running backward pass
+        self._pass_cb_set = False
         self.register_backward_hook()
         self._post_backward_callback_set = False
 
@@ -75,7 +77,8 @@ class DataParallelBucket(nn.Module):
 
     def register_backward_hook(self):
         self.grad_accs = []
-        for param in self.module.parameters():
+        for name, param in self.module.named_parameters():
+            param._pico_name = name  # error messages only
             if param.requires_grad:
                 self.grad_accs.append(param.register_post_accumulate_grad_hook(
                     self._make_param_hook(param, self.bucket_manager)))
@@ -89,12 +92,14 @@ class DataParallelBucket(nn.Module):
 
         def param_hook(*unused):
             # A producer that accumulated into main_grad itself (fused wgrad GEMM, RMSNorm dw, embedding
-            # backward: ops.wgrad_accumulate / _norm_grad_target) hands autograd no gradient and has already
-            # marked the param ready; AccumulateGrad then normally skips its post-accumulate hooks, and if it
-            # does call them there is nothing to add. No state is carried between micro-batches, so a param
-            # may switch between the fused and the hook path at any micro-batch (PICO_WGRAD_FUSION toggled,
-            # a non-contiguous main_grad, TP layers swapped in) without dropping a gradient.
-            if param.grad is None:
+            # backward: ops.wgrad_accumulate / _norm_grad_target) hands autograd no gradient and records the
+            # param in this backward pass's fused set (ready()); AccumulateGrad still calls post-accumulate
+            # hooks for a None gradient, and with persistent .grad buffers (HIP-graph replay, set_to_none=
+            # False) param.grad is not None then, so the set — not the .grad — says there is nothing to add.
+            # The set is cleared at the end of every backward pass, so nothing carries over between
+            # micro-batches: a param may switch between the fused and the hook path at any micro-batch
+            # (PICO_WGRAD_FUSION toggled, a non-contiguous main_grad, TP layers swapped in).
+            if param.grad is None or param in self._fused_pass:
                 return
             if param.requires_grad:
                 sync = self.require_backward_grad_sync
@@ -108,12 +113,20 @@ class DataParallelBucket(nn.Module):
                     bucket_manager.mark_param_as_ready(param, prescaled=True)
         return param_hook
 
+    def _end_pass(self):
+        self._fused_pass.clear()
+        self._pass_cb_set = False
+
     def _wgrad_sync(self):
         return self.require_backward_grad_sync, self.bucket_manager.process_group_size
 
     def _make_ready_fn(self, param, bucket_manager):
         def ready():
             # the GEMM already did main_grad = (main_grad + dW) / W on the syncing micro-batch
+            self._fused_pass.add(param)
+            if not self._pass_cb_set:
+                Variable._execution_engine.queue_callback(self._end_pass)
+                self._pass_cb_set = True
             if self.require_backward_grad_sync:
                 if not self._post_backward_callback_set:
                     Variable._execution_engine.queue_callback(self._post_backward)

@@ -556,9 +556,120 @@ class _LMHeadCEFn(torch.autograd.Function):
         return dx, dw, None, None
 
 
-def lm_head_cross_entropy(x, w, target, ignore_index=-100):
-    """mean cross-entropy of the LM head x W^T against target, fused (_LMHeadCEFn)."""
-    return _LMHeadCEFn.apply(x, w, target, ignore_index)
+class _LMHeadCEChunkedFn(torch.autograd.Function):
+    """grad_scale * mean F.cross_entropy(x W^T, target), chunked over tokens so the [T, V] logits never
+    exist whole (ref picotron/model.py:246,269 + ref train.py:46-49). Per chunk of
+    `chunk` rows, in the FORWARD: logits_c = x_c W^T into one reusable [chunk, V] buffer (100 MB at
+    1024 x 49152 bf16, resident in the 256 MB Infinity Cache instead of a 403 MB HBM round trip), the CE
+    kernel turns it in place into grad_scale * dlogits_c, then dx_c = dlogits_c W and dW += dlogits_c^T x_c
+    (accumulated where wgrad_accumulate would put it: DP main_grad with 1/W folded on the syncing
+    micro-batch, the bf16 .grad, or a buffer handed to autograd). The backward only scales the saved dx
+    by the upstream gradient and marks the weight ready for the DP bucket.
+
+    Contract: grad_scale is the gradient the loss will receive (the training loop's 1 / grad_acc folded
+    in here instead of dividing the loss; loss.backward() then feeds 1). dx stays exact for any upstream
+    gradient; the already-accumulated dW assumes it is 1 (PICO_CHECK_GRAD_SCALE=1 asserts it, with a sync)."""
+
+    @staticmethod
+    def forward(ctx, x, w, target, ignore_index, grad_scale, chunk):
+        _need(x, "x")
+        _need(w, "w")
+        H = x.shape[-1]
+        x2 = x.reshape(-1, H)
+        T, V = x2.shape[0], w.shape[0]
+        t = target.reshape(-1)
+        if t.dtype != torch.int64:
+            t = t.long()
+        t = t.contiguous()
+        n_valid = (t != ignore_index).sum().to(torch.float32)
+        gscale = (float(grad_scale) / n_valid).reshape(1)
+        lse = torch.empty(T, dtype=torch.float32, device=x.device)
+        loss_rows = torch.empty(T, dtype=torch.float32, device=x.device)
+        dx = torch.empty(T, H, dtype=x.dtype, device=x.device)
+        chunk = max(1, min(int(chunk), T))
+        buf = torch.empty(chunk, V, dtype=x.dtype, device=x.device)
+        wt = weight_t(w, (w,)) if wt_dgrad_enabled() else None
+        xin = _wgrad_input(x2, V, x)  # x2, or x2^T's transposed view ("TT" wgrad form)
+        need_w = ctx.needs_input_grad[1]
+        # where dW goes (wgrad_accumulate's targets), decided once for the whole call
+        kind, dst, sc, ready = "autograd", None, 1.0, None
+        if need_w and wgrad_fusion_enabled():
+            mg = getattr(w, "main_grad", None)
+            if mg is not None and getattr(w, "_pico_wgrad_ready", None) is not None:
+                if mg.dtype == torch.float32 and mg.is_contiguous() and tuple(mg.shape) == tuple(w.shape):
+                    sync, world = w._pico_wgrad_sync()
+                    kind, dst, sc, ready = "main", mg, (1.0 / world if sync else 1.0), w._pico_wgrad_ready
+            elif mg is None and not _has_hooks(w) and w.dtype == x.dtype:
+                g = w.grad
+                if g is None:
+                    kind = "fresh"
+                elif g.is_contiguous() and g.dtype == w.dtype and tuple(g.shape) == tuple(w.shape):
+                    kind, dst = "grad", g
+        lib = _lib.load()
+        for c0 in range(0, T, chunk):
+            c1 = min(T, c0 + chunk)
+            n = c1 - c0
+            lg = buf[:n]
+            torch.mm(x2[c0:c1], w.t(), out=lg)
+            _lib.check(lib.pico_cross_entropy_fwd_grad(_lib.ptr(lg), lg.stride(0), _lib.ptr(t[c0:c1]), _lib.ptr(lse[c0:]),
+                                                       _lib.ptr(loss_rows[c0:]), _lib.ptr(gscale), n, V,
+                                                       int(ignore_index), _lib.stream_of(x)),
+                       "pico_cross_entropy_fwd_grad")
+            if ctx.needs_input_grad[0]:
+                if wt is not None:
+                    torch.mm(lg, wt.t(), out=dx[c0:c1])
+                else:
+                    torch.mm(lg, w, out=dx[c0:c1])
+            if not need_w:
+                continue
+            xc = xin[c0:c1]
+            if kind == "main":  # fp32 main_grad: 1/W folds into the first chunk's beta and every alpha
+                torch.addmm(dst, lg.t(), xc, beta=(sc if c0 == 0 else 1.0), alpha=sc, out_dtype=torch.float32, out=dst)
+            elif kind in ("grad", "fresh_acc", "autograd_acc"):
+                torch.addmm(dst, lg.t(), xc, out=dst)
+            elif kind == "fresh":
+                w.grad = dst = torch.mm(lg.t(), xc)
+                kind = "fresh_acc"
+            else:  # "autograd": a buffer handed back from the backward
+                dst = torch.mm(lg.t(), xc)
+                kind = "autograd_acc"
+        loss = loss_rows.sum() / n_valid * grad_scale
+        ctx.save_for_backward(dx)
+        ctx.xshape = x.shape
+        ctx.dw = dst if kind == "autograd_acc" else None
+        ctx.ready = ready
+        return loss.to(x.dtype)
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        (dx,) = ctx.saved_tensors
+        g = grad_out.to(torch.float32)
+        if os.getenv("PICO_CHECK_GRAD_SCALE", "0") == "1":
+            assert float(g) == 1.0, f"lm_head_cross_entropy(grad_scale=...): upstream gradient {float(g)} != 1"
+        dxo = None
+        if ctx.needs_input_grad[0]:
+            dxo = dx.mul_(g).view(ctx.xshape)
+        if ctx.ready is not None:
+            ctx.ready()
+        dw = ctx.dw
+        ctx.dw = None
+        return dxo, dw, None, None, None, None
+
+
+def ce_chunk_rows():
+    """Rows per LM-head CE chunk in the training loop (PICO_CE_CHUNK; 0 = the unchunked fused form)."""
+    return int(os.getenv("PICO_CE_CHUNK", "4096"))
+
+
+def lm_head_cross_entropy(x, w, target, ignore_index=-100, grad_scale=None, chunk=None):
+    """mean cross-entropy of the LM head x W^T against target, fused. grad_scale=None: the drop-in form
+    (_LMHeadCEFn, logits [T, V] kept for the backward GEMMs). grad_scale=s: returns s * mean CE, computed
+    chunk rows at a time with dx and dW in the forward (_LMHeadCEChunkedFn; the loss must then be
+    back-propagated with unit gradient)."""
+    if grad_scale is None:
+        return _LMHeadCEFn.apply(x, w, target, ignore_index)
+    return _LMHeadCEChunkedFn.apply(x, w, target, ignore_index, float(grad_scale),
+                                    ce_chunk_rows() if chunk is None else int(chunk))
 
 
 def cross_entropy(logits, target, ignore_index=-100, reduction="mean"):

@@ -43,7 +43,10 @@ def _micro_batch(model, input_ids, target_ids, grad_acc_steps):
     if head is not None:  # fused LM head + cross-entropy: logits never re-read
         from . import ops
         h = model(input_ids=input_ids, return_hidden=True)
-        loss = ops.lm_head_cross_entropy(h, head.weight, target_ids.reshape(-1)) / grad_acc_steps
+        if ops.ce_chunk_rows() > 0:  # chunked: 1 / grad_acc folded into the op (its dW is taken in the forward)
+            loss = ops.lm_head_cross_entropy(h, head.weight, target_ids.reshape(-1), grad_scale=1.0 / grad_acc_steps)
+        else:
+            loss = ops.lm_head_cross_entropy(h, head.weight, target_ids.reshape(-1)) / grad_acc_steps
     else:
         outputs = model(input_ids=input_ids)
         batch_size, seq_len = input_ids.shape

@@ -115,3 +115,78 @@ def test_dp_sync_semantics(tmp_path):
             name = k[len("main_grad."):]
             assert torch.equal(r0[k], r1[k]), name
             assert float(r0["local." + name].abs().sum()) > 0
+
+
+def _fused_worker(rank, world, port, outdir):
+    """A producer that accumulates into main_grad itself and calls param._pico_wgrad_ready() (as the fused
+    wgrad GEMMs do), next to a plain parameter on the hook path, with persistent .grad buffers
+    (set_to_none=False, as under HIP-graph replay): each param is marked ready exactly once per syncing
+    backward and main_grad holds the micro-batch sum."""
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle import hotpath as H
+    from picotron_amd import process_group_manager as pgm
+    from picotron_amd.data_parallel import bucket as B
+    from picotron_amd.data_parallel.data_parallel import DataParallelBucket
+    pgm.setup_process_group_manager(tp_size=1, cp_size=1, pp_size=1, dp_size=world)
+    B.set_kernels(H.CpuBucketKernels())
+
+    class FusedMul(torch.autograd.Function):  # y = x * w; dw goes straight into w.main_grad
+        @staticmethod
+        def forward(ctx, x, w):
+            ctx.save_for_backward(x)
+            ctx.w = w
+            return x * w
+
+        @staticmethod
+        def backward(ctx, g):
+            (x,) = ctx.saved_tensors
+            w = ctx.w
+            sync, W = w._pico_wgrad_sync()
+            w.main_grad.add_((g * x).sum(0))
+            if sync:
+                w.main_grad.div_(W)
+            w._pico_wgrad_ready()
+            return g * w, None
+
+    class M(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.a = torch.nn.Parameter(torch.ones(4))
+            self.b = torch.nn.Parameter(torch.full((4,), 2.0))
+
+        def forward(self, x):
+            return FusedMul.apply(x, self.a) * self.b
+
+    m = DataParallelBucket(M(), bucket_cap_mb=1)
+    for step in range(2):
+        for p in m.parameters():  # persistent .grad from the second step on
+            if p.grad is not None:
+                p.grad.zero_()
+        # step 1: one syncing micro-batch straight after the persistent .grad views were installed (the
+        # eager micro-batch after graph replays): the hook sees a non-None .grad for the fused param
+        xs = [torch.full((3, 4), float(i + 1 + rank)) for i in range(3 if step == 0 else 1)]
+        for i, x in enumerate(xs):
+            m.require_backward_grad_sync = i == len(xs) - 1
+            m(x).sum().backward()
+        torch.save({"a": m.module.a.main_grad.clone(), "b": m.module.b.main_grad.clone()},
+                   os.path.join(outdir, f"s{step}_r{rank}.pt"))
+        m.reset()
+    dist.destroy_process_group()
+
+
+def test_fused_ready_with_persistent_grads(tmp_path):
+    world = 2
+    mp.start_processes(_fused_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    # d/da sum(x a b) = sum_rows(x) * b = 3 x b; d/db = 3 x a; x = i + 1 + rank, a = 1, b = 2
+    for step in range(2):
+        n = 3 if step == 0 else 1
+        sa = sum(3 * (i + 1 + r) * 2.0 for i in range(n) for r in range(world)) / world
+        sb = sum(3 * (i + 1 + r) * 1.0 for i in range(n) for r in range(world)) / world
+        for r in range(world):
+            got = torch.load(tmp_path / f"s{step}_r{r}.pt", weights_only=True)
+            assert torch.allclose(got["a"], torch.full((4,), sa)), (step, r, got["a"])
+            assert torch.allclose(got["b"], torch.full((4,), sb)), (step, r, got["b"])

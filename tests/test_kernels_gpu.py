@@ -494,6 +494,53 @@ def test_lm_head_cross_entropy_fused(V, ignore, g):
     assert rel_l2(x.grad.cpu(), x2.grad.cpu()) < 1.5e-2
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("T,chunk,V,ignore,mode", [(512, 128, 4000, False, "grad"), (500, 192, 4000, True, "fresh"),
+                                                   (1024, 1024, 49152, True, "grad"), (700, 256, 4000, True, "autograd"),
+                                                   (384, 100, 4000, False, "nograd")])
+def test_lm_head_cross_entropy_chunked(T, chunk, V, ignore, mode):
+    """ops.lm_head_cross_entropy(grad_scale=s, chunk=c) — logits never whole, dx / dW taken chunk by chunk in
+    the forward — == s * mean F.cross_entropy(x W^T) in fp64 with unit upstream gradient: loss, dx, dW
+    accumulated onto an existing bf16 .grad ("grad"), created when .grad is None ("fresh"), handed to
+    autograd when the weight has a hook ("autograd"), or not at all ("nograd": weight frozen); ragged last
+    chunks and ignore_index rows included. It matches the unchunked fused form on the same inputs."""
+    from picotron_amd import ops
+    torch.manual_seed(T + chunk + V)
+    H, s = 256, 0.25
+    x = (torch.randn(T, H, device=DEV) * 0.5).to(BF).requires_grad_(True)
+    w = (torch.randn(V, H, device=DEV) * 0.05).to(BF).requires_grad_(mode != "nograd")
+    w0 = (torch.randn(V, H, device=DEV) * 1e-5).to(BF)
+    if mode == "grad":
+        w.grad = w0.clone()
+    if mode == "autograd":
+        w.register_hook(lambda g: g)
+    tgt = torch.randint(0, V, (T,), device=DEV)
+    if ignore:
+        tgt[::7] = -100
+    loss = ops.lm_head_cross_entropy(x, w, tgt, grad_scale=s, chunk=chunk)
+    loss.backward()
+    xd, wd = x.detach().double().requires_grad_(True), w.detach().double().requires_grad_(True)
+    ref = torch.nn.functional.cross_entropy(xd @ wd.t(), tgt) * s
+    ref.backward()
+    assert loss.dtype == BF
+    assert abs(float(loss) - float(ref)) <= 8e-3 * abs(float(ref)) + 1e-3
+    assert rel_l2(x.grad.cpu(), xd.grad.cpu()) < 1.5e-2
+    if mode != "nograd":
+        got = w.grad.double() - (w0.double() if mode == "grad" else 0)
+        assert rel_l2(got.cpu(), wd.grad.cpu()) < 3e-2
+    else:
+        assert w.grad is None
+    # the unchunked fused form on the same inputs
+    x2 = x.detach().clone().requires_grad_(True)
+    w2 = w.detach().clone().requires_grad_(True)
+    l2 = ops.lm_head_cross_entropy(x2, w2, tgt)
+    (l2 * s).backward()
+    assert abs(float(l2) * s - float(loss)) <= 1e-2 * abs(float(ref)) + 2e-3
+    assert rel_l2(x.grad.cpu(), x2.grad.cpu()) < 1e-2
+    if mode != "nograd":
+        assert rel_l2(got.cpu(), w2.grad.double().cpu()) < 1e-2
+
+
 # ------------------------------------------------------------------------------------------ transpose
 @pytest.mark.parametrize("R,C,ld_pad", [(4096, 2048, 0), (6144, 2048, 0), (2048, 49152, 0), (72, 8, 0),
                                         (8, 136, 0), (200, 264, 16), (64, 64, 8)])

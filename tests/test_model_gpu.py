@@ -212,12 +212,15 @@ def test_fused_paths_match_unfused(golden_loss, monkeypatch):
         assert rel_l2(outs["0"][1][n].cpu(), outs["1"][1][n].cpu()) < 3e-2, n
 
 
-def test_micro_batch_fused_lm_head_ce(golden_loss, monkeypatch):
+@pytest.mark.parametrize("chunk", ["0", "96"])
+def test_micro_batch_fused_lm_head_ce(golden_loss, monkeypatch, chunk):
     """train._micro_batch with the fused LM head + cross-entropy == the logits + CE path (loss and every
-    parameter's accumulated gradient, 2 micro-batches of grad_acc 2, within bf16 tolerance)."""
+    parameter's accumulated gradient, 2 micro-batches of grad_acc 2, within bf16 tolerance); unchunked
+    (PICO_CE_CHUNK=0) and chunked over 96-row pieces (dx / dW in the forward, 1/grad_acc folded in)."""
     from picotron_amd import train
     from picotron_amd.model import build_llama
     from conftest import rel_l2
+    monkeypatch.setenv("PICO_CE_CHUNK", chunk)
     cfg = _cfg(golden_loss)
     g = torch.Generator("cuda").manual_seed(17)
     toks = [torch.randint(0, cfg.vocab_size, (2, 129), device="cuda", generator=g) for _ in range(2)]
