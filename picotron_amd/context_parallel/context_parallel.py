@@ -11,7 +11,13 @@ Differences (MI355X-native, same numbers):
   * the interface keeps the reference's layout — q/k/v and the output are [B, H, S, D] (ref :14-15, caller
     ref picotron/model.py:147-150) — but internally the blocks run on [B, S, H, D] views of the same
     storage (a transpose view, no copy), the kernels' native layout;
-  * the ring transport waits on its requests only (no device-wide synchronize per step).
+  * the ring transport waits on its requests only (no device-wide synchronize per step);
+  * optional zig-zag load balancing (PICO_CP_ZIGZAG=1; the reference's TODO at
+    ref tests/test_dataloader.py:136): the sequence is cut into 2 * cp chunks and cp rank r holds chunks
+    r and 2 cp - 1 - r, so with a causal mask every rank does the same work at every ring step — the
+    reference's contiguous split leaves rank r with r + 1 of cp block products (rank cp - 1 does cp,
+    rank 0 one). The loader (data.py), the RoPE slice (update_rope_for_context_parallel) and the ring
+    (RingAttentionFunc) switch together; zigzag_positions() is the one definition of the layout.
 """
 import os
 
@@ -23,9 +29,27 @@ from .. import process_group_manager as pgm
 from .cp_communications import ContextCommunicate
 
 
-def apply_context_parallel(model):
+def apply_context_parallel(model, zigzag=None):
     os.environ["CONTEXT_PARALLEL"] = "1" if pgm.process_group_manager.cp_world_size > 1 else "0"
+    if zigzag is not None:
+        os.environ["PICO_CP_ZIGZAG"] = "1" if zigzag else "0"
     return model
+
+
+def zigzag_enabled():
+    return os.getenv("PICO_CP_ZIGZAG", "0") == "1"
+
+
+def zigzag_positions(seq_len, cp_rank, cp_world_size):
+    """Global token positions held by `cp_rank` under the zig-zag split: chunk r, then chunk 2 cp - 1 - r
+    (chunk = seq_len / (2 cp)); increasing, so a causal mask over the local sequence is the global one
+    restricted to it."""
+    assert seq_len % (2 * cp_world_size) == 0, \
+        f"zig-zag context parallelism needs seq_len ({seq_len}) divisible by 2 * cp ({2 * cp_world_size})"
+    c = seq_len // (2 * cp_world_size)
+    first = torch.arange(cp_rank * c, (cp_rank + 1) * c)
+    second = torch.arange((2 * cp_world_size - 1 - cp_rank) * c, (2 * cp_world_size - cp_rank) * c)
+    return torch.cat([first, second])
 
 
 def ring_attention(q, k, v, sm_scale, is_causal):
@@ -63,6 +87,14 @@ class RingAttentionFunc(torch.autograd.Function):
     @staticmethod
     def forward(ctx, q, k, v, sm_scale, is_causal):
         comm = ContextCommunicate("comm")
+        zz = is_causal and zigzag_enabled() and comm.world_size > 1
+        ctx.zigzag = zz
+        if zz:
+            out, lse = RingAttentionFunc._zigzag_forward(comm, q, k, v, sm_scale)
+            ctx.save_for_backward(q, k, v, out, lse)
+            ctx.sm_scale = sm_scale
+            ctx.is_causal = is_causal
+            return out
         k_og, v_og = k, v
         out, lse = None, None
         for step in range(comm.world_size):
@@ -83,11 +115,47 @@ class RingAttentionFunc(torch.autograd.Function):
         return out
 
     @staticmethod
+    def _zigzag_forward(comm, q, k, v, sm_scale):
+        """Local rows = [chunk r | chunk 2n-1-r], each c long. Step 0 (own K/V): causal over the local rows.
+        K/V from rank src < r: both query chunks see src's first chunk only (its second lies after both):
+        all rows x first c keys. From src > r: only the second query chunk sees anything, and all of it:
+        last c rows x all keys. Every step after the first is c x 2c, on every rank."""
+        c = q.shape[1] // 2
+        r, n = comm.rank, comm.world_size
+        halves = [[None, None], [None, None]]  # running fp32 (out, lse) of query chunks 0 and 1
+
+        def merge(h, bo, bl):
+            halves[h][0], halves[h][1] = update_out_and_lse(halves[h][0], halves[h][1], bo, bl.contiguous())
+
+        for step in range(n):
+            if step + 1 != n:
+                next_k = comm.send_recv(k)
+                next_v = comm.send_recv(v)
+                comm.commit()
+            src = (r - step) % n
+            if step == 0 or src < r:
+                kk, vv = (k, v) if step == 0 else (k[:, :c], v[:, :c])
+                bo, bl = ops.attention_block_fwd(q, kk, vv, sm_scale, step == 0)
+                merge(0, bo[:, :c], bl[:, :, :c])
+                merge(1, bo[:, c:], bl[:, :, c:])
+            else:
+                bo, bl = ops.attention_block_fwd(q[:, c:], k, v, sm_scale, False)
+                merge(1, bo, bl)
+            if step + 1 != n:
+                comm.wait()
+                k, v = next_k, next_v
+        out = torch.cat([halves[0][0], halves[1][0]], 1).to(q.dtype)
+        lse = torch.cat([halves[0][1], halves[1][1]], 2)
+        return out, lse
+
+    @staticmethod
     def backward(ctx, dout, *args):
         q, k, v, out, lse = ctx.saved_tensors
         sm_scale, is_causal = ctx.sm_scale, ctx.is_causal
         kv_comm = ContextCommunicate("kv_comm")
         d_kv_comm = ContextCommunicate("d_kv_comm")
+        if ctx.zigzag:
+            return RingAttentionFunc._zigzag_backward(kv_comm, d_kv_comm, dout, q, k, v, out, lse, sm_scale)
         dq = torch.zeros(q.shape, dtype=torch.float32, device=q.device)
         dk = dv = None
         next_dk = next_dv = None
@@ -118,11 +186,58 @@ class RingAttentionFunc(torch.autograd.Function):
         d_kv_comm.wait()
         return dq.to(q.dtype), next_dk.to(q.dtype), next_dv.to(q.dtype), None, None
 
+    @staticmethod
+    def _zigzag_backward(kv_comm, d_kv_comm, dout, q, k, v, out, lse, sm_scale):
+        """Block backwards from the GLOBAL O / LSE in the forward's zig-zag pattern; the partial dK/dV of
+        the K/V block in hand travels the ring with it and returns complete to its owner."""
+        c = q.shape[1] // 2
+        r, n = kv_comm.rank, kv_comm.world_size
+        dout = dout.contiguous()
+        dq = torch.zeros(q.shape, dtype=torch.float32, device=q.device)
+        lse1 = lse[:, :, c:].contiguous()
+        dk = dv = next_dk = next_dv = None
+        for step in range(n):
+            if step + 1 != n:
+                next_k = kv_comm.send_recv(k)
+                next_v = kv_comm.send_recv(v)
+                kv_comm.commit()
+            src = (r - step) % n
+            if step == 0:
+                _, bdk, bdv = ops.attention_block_bwd(dout, q, k, v, out, lse, sm_scale, True, dq_accum=dq)
+                dk, dv = bdk.float(), bdv.float()
+            else:
+                if src < r:  # all local rows x the first c keys of src
+                    _, bdk, bdv = ops.attention_block_bwd(dout, q, k[:, :c], v[:, :c], out, lse, sm_scale, False,
+                                                          dq_accum=dq)
+                else:        # the last c local rows x all keys of src
+                    _, bdk, bdv = ops.attention_block_bwd(dout[:, c:], q[:, c:], k, v, out[:, c:], lse1, sm_scale,
+                                                          False, dq_accum=dq[:, c:])
+                d_kv_comm.wait()
+                dk, dv = next_dk, next_dv
+                if src < r:
+                    dk[:, :c] += bdk
+                    dv[:, :c] += bdv
+                else:
+                    dk += bdk
+                    dv += bdv
+            if step + 1 != n:
+                kv_comm.wait()
+                k, v = next_k, next_v
+            next_dk = d_kv_comm.send_recv(dk)
+            next_dv = d_kv_comm.send_recv(dv)
+            d_kv_comm.commit()
+        d_kv_comm.wait()
+        return dq.to(q.dtype), next_dk.to(q.dtype), next_dv.to(q.dtype), None, None
+
 
 def update_rope_for_context_parallel(cos, sin):
-    """Slice the RoPE tables to this cp rank's contiguous sequence chunk (ref :189-195)."""
+    """Slice the RoPE tables to this cp rank's contiguous sequence chunk (ref :189-195), or to its two
+    zig-zag chunks (PICO_CP_ZIGZAG=1)."""
     seq_len, _ = cos.size()
     cp_rank, cp_world_size = pgm.cp_rank_and_size()
+    if zigzag_enabled() and cp_world_size > 1:
+        idx = zigzag_positions(seq_len, cp_rank, cp_world_size).to(cos.device)
+        return cos.index_select(0, idx), sin.index_select(0, idx)
     assert seq_len % cp_world_size == 0, \
         f"Input sequence length ({seq_len}) must be divisible by cp_world_size ({cp_world_size})"
     size = seq_len // cp_world_size

@@ -9,6 +9,8 @@ deterministically per (seed, dp_rank, step):
   * "arith":   tok[t] = (start + stride * t) mod vocab with random start/stride per row — a learnable
                stream for loss-curve overlays.
 """
+import os
+
 import torch
 
 from . import process_group_manager as pgm
@@ -52,7 +54,17 @@ class SyntheticDataLoader:
         return synth_tokens(self.micro_batch_size, self.seq_length + 1, self.vocab_size, self._gen, self.kind)
 
     def collate(self, tokens):
-        """CP slicing of ref picotron/data.py:102-116."""
+        """CP slicing of ref picotron/data.py:102-116 (zig-zag chunks with PICO_CP_ZIGZAG=1)."""
+        if self.cp_world_size > 1 and os.getenv("PICO_CP_ZIGZAG", "0") == "1":
+            from .context_parallel.context_parallel import zigzag_positions
+            pos = zigzag_positions(self.seq_length, self.cp_rank, self.cp_world_size)
+            B = tokens.size(0)
+            return {
+                "input_ids": tokens[:, pos].contiguous(),
+                "target_ids": tokens[:, pos + 1].contiguous(),
+                "position_ids": pos.unsqueeze(0).expand(B, -1).contiguous(),
+                "hidden_states": None,
+            }
         start = self.cp_rank * self.seq_length_per_gpu
         end = start + self.seq_length_per_gpu
         B = tokens.size(0)

@@ -53,7 +53,7 @@ def _staged_comm_class(base):
     return HostStagedCommunicate
 
 
-def _worker(rank, world, port, causal):
+def _worker(rank, world, port, causal, zigzag=False):
     import sys
     sys.path.insert(0, ROOT)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -64,6 +64,7 @@ def _worker(rank, world, port, causal):
     from picotron_amd import process_group_manager as pgm
     from picotron_amd.context_parallel import context_parallel as CP
     pgm.setup_process_group_manager(tp_size=1, cp_size=world, pp_size=1, dp_size=1)
+    os.environ["PICO_CP_ZIGZAG"] = "1" if zigzag else "0"
     CP.ContextCommunicate = _staged_comm_class(CP.ContextCommunicate)
 
     dev = "cuda:0"
@@ -76,7 +77,8 @@ def _worker(rank, world, port, causal):
     of = ops.flash_attn_func(qf, kf, vf, softmax_scale=scale, causal=causal)
     of.backward(do)
     n = S // world
-    sl = slice(rank * n, (rank + 1) * n)
+    # this rank's rows: contiguous chunk (reference split) or the zig-zag pair of chunks
+    sl = CP.zigzag_positions(S, rank, world).to(dev) if zigzag else slice(rank * n, (rank + 1) * n)
     ql, kl, vl = [t[:, sl].contiguous().requires_grad_(True) for t in (q, k, v)]
     # exactly the reference's call (ref picotron/model.py:139-150): [B, S, H, D] projections transposed to
     # [B, H, S, D], ring_attention, output transposed back to [B, S, H, D]
@@ -97,9 +99,14 @@ def _worker(rank, world, port, causal):
     dist.barrier()
     dist.destroy_process_group()
     if bad:
-        raise AssertionError(f"rank {rank} cp={world} causal={causal}: {bad} (all: {errs})")
+        raise AssertionError(f"rank {rank} cp={world} causal={causal} zigzag={zigzag}: {bad} (all: {errs})")
 
 
-@pytest.mark.parametrize("world,causal", [(2, True), (4, True), (2, False)])
-def test_ring_attention_multi_rank(world, causal):
-    mp.start_processes(_worker, args=(world, _free_port(), causal), nprocs=world, join=True, start_method="spawn")
+@pytest.mark.parametrize("world,causal,zigzag", [(2, True, False), (4, True, False), (2, False, False),
+                                                 (2, True, True), (4, True, True)])
+def test_ring_attention_multi_rank(world, causal, zigzag):
+    """Contiguous (reference) split, and the zig-zag split (PICO_CP_ZIGZAG=1: rank r holds chunks r and
+    2 cp - 1 - r; every rank does equal block work), against whole-sequence attention at the rows each
+    rank holds."""
+    mp.start_processes(_worker, args=(world, _free_port(), causal, zigzag), nprocs=world, join=True,
+                       start_method="spawn")
