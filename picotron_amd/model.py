@@ -85,6 +85,26 @@ def flash_attention(q, k, v, causal=True):
     return ops.flash_attn_func(q.permute(0, 2, 1, 3), k.permute(0, 2, 1, 3), v.permute(0, 2, 1, 3), causal=causal)
 
 
+def _col_parallel(mods):
+    """'tp' if every module is a bias-free ColumnParallelLinear shard the fused ops can take (its f region
+    — the input-gradient all-reduce — applied once by the caller), 'plain' if every one is a bias-free
+    nn.Linear, else None."""
+    from .tensor_parallel.tensor_parallel import ColumnParallelLinear
+    if all(type(m) is nn.Linear and m.bias is None for m in mods):
+        return "plain"
+    if all(type(m) is ColumnParallelLinear and m.bias is None and not m.gather_output and not m.async_all_reduce
+           for m in mods):
+        return "tp"
+    return None
+
+
+def _tp_input(kind, x):
+    if kind == "tp" and pgm.process_group_manager is not None and pgm.process_group_manager.tp_world_size > 1:
+        from .tensor_parallel.tp_communications import CopyToModelParallelRegion
+        return CopyToModelParallelRegion.apply(x)
+    return x
+
+
 def _proj(mod, x):
     """A projection: bias-free nn.Linear runs ops.linear (gradient-accumulation fusion); anything
     else (TP-parallel layers, biases) runs as is."""
@@ -148,14 +168,18 @@ class Attention(nn.Module):
             torch.nn.init.uniform_(w, -bound, bound)
 
     def _fusable(self):
-        return (os.getenv("CONTEXT_PARALLEL", "0") != "1" and os.getenv("PICO_UNFUSED", "0") != "1"
-                and all(type(m) is nn.Linear and m.bias is None for m in (self.q_proj, self.k_proj, self.v_proj)))
+        if os.getenv("CONTEXT_PARALLEL", "0") == "1" or os.getenv("PICO_UNFUSED", "0") == "1":
+            return None
+        return _col_parallel((self.q_proj, self.k_proj, self.v_proj))
 
     def forward(self, x, cos, sin, attention_mask=None, position_ids=None):
         B, S, _ = x.size()
         D = self.head_dim
-        if self._fusable():
-            # one q|k|v GEMM, RoPE in place on q|k, attention on strided views (ops._QKVRopeAttentionFn)
+        kind = self._fusable()
+        if kind is not None:
+            # one q|k|v GEMM, RoPE in place on q|k, attention on strided views (ops._QKVRopeAttentionFn);
+            # under TP the local shards, with one f region (input-gradient all-reduce) for all three
+            x = _tp_input(kind, x)
             out = ops.qkv_rope_attention(x, self.q_proj.weight, self.k_proj.weight, self.v_proj.weight, cos, sin,
                                          self.num_local_heads, self.num_local_kv_heads, True)
             return _proj(self.out_proj, out)
@@ -192,9 +216,10 @@ class MLP(nn.Module):
             torch.nn.init.uniform_(w, -bound, bound)
 
     def forward(self, x):
-        if (os.getenv("PICO_UNFUSED", "0") != "1" and type(self.gate_proj) is nn.Linear
-                and type(self.up_proj) is nn.Linear and self.gate_proj.bias is None and self.up_proj.bias is None):
-            # one gate|up GEMM + strided SwiGLU (ops._GateUpSwiGLUFn)
+        kind = _col_parallel((self.gate_proj, self.up_proj)) if os.getenv("PICO_UNFUSED", "0") != "1" else None
+        if kind is not None:
+            # one gate|up GEMM + strided SwiGLU (ops._GateUpSwiGLUFn); under TP on the local shards, one f region
+            x = _tp_input(kind, x)
             return _proj(self.down_proj, ops.gate_up_swiglu(x, self.gate_proj.weight, self.up_proj.weight))
         return self.down_proj(ops.swiglu(self.gate_proj(x), self.up_proj(x)))
 

@@ -1,10 +1,10 @@
-"""The hot path as a drop-in under tensor parallelism (north_star: "tensor_parallel ... run it as a
-drop-in"): tp = 2 ranks sharing this GPU (gloo; RCCL refuses two ranks on one device) replace the
-decoder layers' projections by attribute name with column / row parallel layers, the way the
-reference's apply_tensor_parallel does (ref picotron/tensor_parallel/tensor_parallel.py:9-51:
-q/k/v/up/gate column-parallel, out/down row-parallel). The layers below are a minimal test-side
-restatement of those wrappers (the reference is a caller, not rebuilt; it never runs on the GPU box).
-Forward logits, loss and every gradient must match the unsharded model on the same weights.
+"""The hot path under tensor parallelism: tp = 2 ranks sharing this GPU (gloo; RCCL refuses two ranks on
+one device) run picotron_amd.tensor_parallel.apply_tensor_parallel (ref picotron/tensor_parallel/
+tensor_parallel.py:9-51: q/k/v/up/gate column-parallel, out/down row-parallel, vocab-parallel embedding,
+gathered LM head) on a model built with the same weights as an unsharded one (shard_weights=True), with
+the fused q|k|v + RoPE + attention and gate|up + SwiGLU paths on the local shards (one f region each) and
+with the unfused per-projection path (PICO_UNFUSED=1). Forward logits, loss and every gradient must match
+the unsharded model.
 """
 import os
 import socket
@@ -26,57 +26,11 @@ def _free_port():
     return p
 
 
-def _tp_layers(group):
-    import torch.distributed as dist
-    import torch.nn.functional as F
-
-    class _CopyToTP(torch.autograd.Function):  # identity forward, all-reduce backward
-        @staticmethod
-        def forward(ctx, x):
-            return x
-
-        @staticmethod
-        def backward(ctx, g):
-            g32 = g.float()  # sum in fp32 (gloo), one rounding back to the activation dtype
-            dist.all_reduce(g32, group=group)
-            return g32.to(g.dtype)
-
-    class _ReduceFromTP(torch.autograd.Function):  # all-reduce forward, identity backward
-        @staticmethod
-        def forward(ctx, x):
-            x32 = x.float()
-            dist.all_reduce(x32, group=group)
-            return x32.to(x.dtype)
-
-        @staticmethod
-        def backward(ctx, g):
-            return g
-
-    class ColumnParallel(torch.nn.Module):
-        def __init__(self, full, rank, world):
-            super().__init__()
-            n = full.out_features // world
-            self.weight = torch.nn.Parameter(full.weight.detach()[rank * n:(rank + 1) * n].clone())
-
-        def forward(self, x):
-            return F.linear(_CopyToTP.apply(x), self.weight)
-
-    class RowParallel(torch.nn.Module):
-        def __init__(self, full, rank, world):
-            super().__init__()
-            n = full.in_features // world
-            self.weight = torch.nn.Parameter(full.weight.detach()[:, rank * n:(rank + 1) * n].clone())
-
-        def forward(self, x):
-            return _ReduceFromTP.apply(F.linear(x, self.weight))
-
-    return ColumnParallel, RowParallel
-
-
-def _worker(rank, world, port):
+def _worker(rank, world, port, unfused):
     import sys
     sys.path.insert(0, ROOT)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ["PICO_UNFUSED"] = "1" if unfused else "0"
     import torch.distributed as dist
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -99,14 +53,10 @@ def _worker(rank, world, port):
         full.final_proj.weight.copy_((torch.randn(full.final_proj.weight.shape, generator=g) * 0.02).to(bf))
         for pf, pt in zip(full.parameters(), tpm.parameters()):
             pt.copy_(pf)
-    Col, Row = _tp_layers(pgm.process_group_manager.tp_group)
-    names = [("attention", "q_proj", Col), ("attention", "k_proj", Col), ("attention", "v_proj", Col),
-             ("attention", "out_proj", Row), ("mlp", "up_proj", Col), ("mlp", "gate_proj", Col),
-             ("mlp", "down_proj", Row)]
-    for lf, lt in zip(full.decoder_layers, tpm.decoder_layers):
-        for mod, attr, cls in names:
-            setattr(getattr(lt, mod), attr, cls(getattr(getattr(lf, mod), attr), rank, world))
-    tpm.to("cuda")
+    from picotron_amd.tensor_parallel.tensor_parallel import apply_tensor_parallel
+    apply_tensor_parallel(tpm, shard_weights=True)
+    if os.environ.get("PICO_UNFUSED", "0") != "1":  # the fused paths take the column-parallel shards
+        assert tpm.decoder_layers[0].attention._fusable() == "tp"
     toks = torch.randint(0, cfg.vocab_size, (2, 129), generator=g).to("cuda")
 
     def run(m):
@@ -142,5 +92,6 @@ def _worker(rank, world, port):
         raise AssertionError(f"rank {rank}: {bad}")
 
 
-def test_tensor_parallel_drop_in():
-    mp.start_processes(_worker, args=(2, _free_port()), nprocs=2, join=True, start_method="spawn")
+@pytest.mark.parametrize("unfused", [False, True])
+def test_tensor_parallel_drop_in(unfused):
+    mp.start_processes(_worker, args=(2, _free_port(), unfused), nprocs=2, join=True, start_method="spawn")
