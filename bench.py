@@ -125,10 +125,14 @@ def main():
     # BASELINE.md's CPU plan, DP = 2 x 4 threads, SmolLM-1.7B geometry 2 layers, seq 1024 (oracle/cpu_baseline.py)
     cpu_baseline = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        from oracle.cpu_baseline import dp2_cpu_throughput
+        from oracle.cpu_baseline import c1_cpu_throughput, dp2_cpu_throughput
         t0 = time.time()
         cpu_baseline = dp2_cpu_throughput()
-        log(f"[rank 0] cpu baseline {cpu_baseline['value']} tok/s ({time.time() - t0:.0f}s)")
+        log(f"[rank 0] cpu baseline DP=2 {cpu_baseline['value']} tok/s ({time.time() - t0:.0f}s)")
+        t0 = time.time()
+        # the plan's other config, C1 (dp2 tp2 pp2 1F1B, 8 ranks x 1 thread), reported beside it
+        cpu_baseline["c1"] = c1_cpu_throughput()
+        log(f"[rank 0] cpu baseline C1 {cpu_baseline['c1']['value']} tok/s ({time.time() - t0:.0f}s)")
     # one GPU per rank; ranks beyond the visible GPUs share them round-robin (gloo rehearsal only)
     device = torch.device("cuda", local_rank % torch.cuda.device_count())
     torch.cuda.set_device(device)

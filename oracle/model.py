@@ -35,13 +35,17 @@ def _uniform_init(w):
 
 
 class Attention(nn.Module):
-    """ref picotron/model.py:87-161, eager branch (SDPA + eager rotary), tp = 1."""
+    """ref picotron/model.py:87-161, eager branch (SDPA + eager rotary). cfg.tp_size (default 1): local
+    head counts of a tensor-parallel rank (ref :95-96), once apply_tensor_parallel has sharded q/k/v/out."""
 
     def __init__(self, cfg):
         super().__init__()
+        tp = getattr(cfg, "tp_size", 1)
         self.num_heads = cfg.num_attention_heads
         self.num_kv = cfg.num_key_value_heads
         self.head_dim = cfg.hidden_size // self.num_heads
+        self.num_local_heads = self.num_heads // tp
+        self.num_local_kv = self.num_kv // tp
         self.q_proj = nn.Linear(cfg.hidden_size, self.num_heads * self.head_dim, bias=False)
         self.k_proj = nn.Linear(cfg.hidden_size, self.num_kv * self.head_dim, bias=False)
         self.v_proj = nn.Linear(cfg.hidden_size, self.num_kv * self.head_dim, bias=False)
@@ -54,16 +58,16 @@ class Attention(nn.Module):
     def forward(self, x, cos, sin):
         B, S, _ = x.shape
         D = self.head_dim
-        q = self.q_proj(x).view(B, S, self.num_heads, D).transpose(1, 2)
-        k = self.k_proj(x).view(B, S, self.num_kv, D).transpose(1, 2)
-        v = self.v_proj(x).view(B, S, self.num_kv, D).transpose(1, 2)
+        q = self.q_proj(x).view(B, S, self.num_local_heads, D).transpose(1, 2)
+        k = self.k_proj(x).view(B, S, self.num_local_kv, D).transpose(1, 2)
+        v = self.v_proj(x).view(B, S, self.num_local_kv, D).transpose(1, 2)
         q = hotpath.rope_eager(q, cos, sin)
         k = hotpath.rope_eager(k, cos, sin)
-        g = self.num_heads // self.num_kv
+        g = self.num_local_heads // self.num_local_kv
         k = k.repeat_interleave(g, dim=1)
         v = v.repeat_interleave(g, dim=1)
         out = F.scaled_dot_product_attention(q, k, v, is_causal=True)
-        return self.out_proj(out.transpose(1, 2).reshape(B, S, self.num_heads * D))
+        return self.out_proj(out.transpose(1, 2).reshape(B, S, self.num_local_heads * D))
 
 
 class MLP(nn.Module):
@@ -103,6 +107,7 @@ class DecoderLayer(nn.Module):
 class Embedding(nn.Module):
     def __init__(self, n, d):
         super().__init__()
+        self.num_embeddings, self.embedding_dim = n, d
         self.weight = nn.Parameter(torch.empty(n, d))
 
     def reset_parameters(self):
