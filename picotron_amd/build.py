@@ -28,6 +28,7 @@ CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno
 # (cdna_hip_programming.md / MI355X_MICROARCH.md: packed f32 ops are an anti-lever there)
 FILE_FLAGS = {
     "attn_bwd_split.hip": ["-fno-slp-vectorize", "-mllvm", "-amdgpu-mfma-vgpr-form"],
+    "attn_fwd.hip": ["-fno-slp-vectorize"],
 }
 
 

@@ -218,7 +218,7 @@ __attribute__((amdgpu_waves_per_eu(FwdCfg<D>::WAVES_PER_EU, FwdCfg<D>::WAVES_PER
     float pv[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) pv[j] = p[j];
-    const bf16x8 pf0 = pack_frag(pv), pf1 = pack_frag(pv + 8);
+    const bf16x8 pf0 = pack_bf16x8(pv), pf1 = pack_bf16x8(pv + 8);  // one v_cvt_pk_bf16_f32 per pair
     lds_wait_all();
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) o[dt] = mfma32(vf[0][dt], pf0, o[dt]);
@@ -327,35 +327,46 @@ __attribute__((amdgpu_waves_per_eu(FwdCfg<D>::WAVES_PER_EU, FwdCfg<D>::WAVES_PER
   }
 
   // ---- epilogue: O = O^T / l, LSE = (m + log2 l) * ln2 ----
+  // Every lane stays (the 16-byte O stores exchange half-chunks between lanes l and l + 32; only rows
+  // < Sq store). O^T (for the out-projection's wgrad) is staged transposed in the now idle LDS ring,
+  // [D][BM + 8], and leaves as 16-byte segments of 8 tokens (instead of 2-byte stores per element).
   const float l_tot = halves_sum(l_i);
-  if (my_q < Sq) {
-    const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
-    bf16_t* op = (bf16_t*)a.o + b * a.o_strides[0] + hq * a.o_strides[2] + (int64_t)my_q * a.o_strides[1];
+  const bool row_ok = my_q < Sq;
+  const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
+  {
+    bf16_t* op = (bf16_t*)a.o + b * a.o_strides[0] + hq * a.o_strides[2] + (int64_t)min(my_q, Sq - 1) * a.o_strides[1];
+    store_row_bf16_x16<DT>(op, h, row_ok, [&](int dt, int i) { return o[dt][i] * inv; });
+  }
+  if (a.o_t) {  // uniform: O^T [Hq*D][tokens]
+    constexpr int TP = BM + 8;  // pitch (elements) of the transposed staging tile
+    static_assert(D * TP * 2 <= C::NBUF * C::SLOT, "O^T staging tile must fit the ring");
+    unsigned short* tt = reinterpret_cast<unsigned short*>(smem);
+    __syncthreads();  // every wave is past its last ring read
 #pragma unroll
-    for (int dt = 0; dt < DT; ++dt) {
+    for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        // registers 4g..4g+3 hold d = 32 dt + 8 g + 4 h + 0..3
-        u16x4 w;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) w[j] = f2bf(o[dt][4 * g + j] * inv);
-        *reinterpret_cast<u16x4*>(op + 32 * dt + 8 * g + 4 * h) = w;
+      for (int i = 0; i < 16; ++i) {
+        const int d = 32 * dt + 8 * (i >> 2) + 4 * h + (i & 3);
+        tt[d * TP + 32 * wave + r] = f2bf(o[dt][i] * inv);
+      }
+    __syncthreads();
+    bf16_t* otb = (bf16_t*)a.o_t + (int64_t)hq * D * a.o_t_ld + (int64_t)b * Sq;
+    const bool vec = ((a.o_t_ld | (int64_t)Sq | (int64_t)(uintptr_t)a.o_t) & 7) == 0;
+    for (int seg = threadIdx.x; seg < D * BM / 8; seg += 256) {
+      const int d = seg / (BM / 8), t8 = seg % (BM / 8);
+      const int tok0 = q0 + 8 * t8;
+      bf16_t* dst = otb + (int64_t)d * a.o_t_ld + tok0;
+      const unsigned short* src = tt + d * TP + 8 * t8;
+      if (vec && tok0 + 8 <= Sq) {
+        *reinterpret_cast<u16x8*>(dst) = *reinterpret_cast<const u16x8*>(src);
+      } else {
+        for (int j = 0; j < 8 && tok0 + j < Sq; ++j) dst[j] = src[j];
       }
     }
-    if (a.o_t) {  // uniform: O^T [Hq*D][tokens]; lanes r = 0..31 are consecutive tokens (64-B segments)
-      bf16_t* ot = (bf16_t*)a.o_t + (int64_t)hq * D * a.o_t_ld + (int64_t)b * Sq + my_q;
-#pragma unroll
-      for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int d = 32 * dt + 8 * (i >> 2) + 4 * h + (i & 3);
-          ot[(int64_t)d * a.o_t_ld] = f2bf(o[dt][i] * inv);
-        }
-    }
-    if (h == 0) {
-      const float lse = l_tot > 0.f ? (m_i + __log2f(l_tot)) * LN2 : -INFINITY;
-      a.lse[((int64_t)b * a.heads_q + hq) * Sq + my_q] = lse;
-    }
+  }
+  if (h == 0 && row_ok) {
+    const float lse = l_tot > 0.f ? (m_i + __log2f(l_tot)) * LN2 : -INFINITY;
+    a.lse[((int64_t)b * a.heads_q + hq) * Sq + my_q] = lse;
   }
 }
 

@@ -83,7 +83,15 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd_kernel(const bf16_t* __restri
 #ifndef PICO_RMS_FWDT_WAVES
 #define PICO_RMS_FWDT_WAVES 8
 #endif
-constexpr int FWDT_WAVES = PICO_RMS_FWDT_WAVES;  // waves per 32-row tile (rows per wave = 32 / FWDT_WAVES)
+// rows per tile: 32 (128 workgroups at 4096 rows: half the CUs) or 16 (256 workgroups); with 16, the two
+// tiles whose y^T segments share each 64-byte line run on one XCD (blocks b and b + 8), so its L2 can merge
+// the two 32-byte halves before they reach HBM
+#ifndef PICO_RMS_FWDT_ROWS
+#define PICO_RMS_FWDT_ROWS 16
+#endif
+constexpr int FWDT_WAVES = PICO_RMS_FWDT_WAVES;  // waves per tile (rows per wave = FWDT_ROWS / FWDT_WAVES)
+constexpr int FWDT_ROWS = PICO_RMS_FWDT_ROWS;
+static_assert(FWDT_ROWS == 16 || FWDT_ROWS == 32, "tile rows");
 
 template <int MAXC, bool RES>
 __global__ __launch_bounds__(FWDT_WAVES * 64) void rmsnorm_fwd_t_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
@@ -91,10 +99,16 @@ __global__ __launch_bounds__(FWDT_WAVES * 64) void rmsnorm_fwd_t_kernel(const bf
                                                             bf16_t* __restrict__ res_out, float* __restrict__ rstd,
                                                             bf16_t* __restrict__ yt, int64_t ldt, float eps) {
   constexpr int COLS = MAXC * 512, PITCH = COLS + 8;
-  extern __shared__ __attribute__((aligned(16))) unsigned short tile[];  // [32][PITCH]
+  extern __shared__ __attribute__((aligned(16))) unsigned short tile[];  // [FWDT_ROWS][PITCH]
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int64_t r0 = (int64_t)blockIdx.x * 32;
-  constexpr int RPW = 32 / FWDT_WAVES;  // rows per wave (rows wid + FWDT_WAVES k): every load issued first
+  int64_t tidx = blockIdx.x;
+  if (FWDT_ROWS == 16 && (gridDim.x & 15) == 0) {  // blocks b, b + 8 (one XCD): tile pair (2p, 2p + 1) of one y^T line
+    const int64_t b = blockIdx.x, g = b >> 4;
+    const int xcd = (int)(b & 7), half = (int)((b >> 3) & 1);
+    tidx = 2 * (g * 8 + xcd) + half;
+  }
+  const int64_t r0 = tidx * FWDT_ROWS;
+  constexpr int RPW = FWDT_ROWS / FWDT_WAVES;  // rows per wave (rows wid + FWDT_WAVES k): every load issued first
   u16x8 xr[RPW][MAXC], rr[RPW][MAXC];
 #pragma unroll
   for (int k = 0; k < RPW; ++k) {
@@ -150,8 +164,9 @@ __global__ __launch_bounds__(FWDT_WAVES * 64) void rmsnorm_fwd_t_kernel(const bf
   }
   __syncthreads();
   // a task = 2 adjacent columns x 8 tokens: 8 dword LDS reads -> two 16-byte y^T segments
-  for (int task = threadIdx.x; task < COLS * 2; task += FWDT_WAVES * 64) {
-    const int cp = task >> 2, part = task & 3;
+  constexpr int NPART = FWDT_ROWS / 8;
+  for (int task = threadIdx.x; task < COLS / 2 * NPART; task += FWDT_WAVES * 64) {
+    const int cp = task / NPART, part = task % NPART;
     u16x8 o0, o1;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -346,8 +361,8 @@ int pico_rmsnorm_fwd_t(const void* x, const void* residual, const void* weight, 
   PICO_REQUIRE(rows / 32 < (1ll << 31), "pico_rmsnorm_fwd_t: too many rows");
   if (rows == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
-  const int nb = (int)(rows / 32);
-  const size_t lds = 32 * (cols + 8) * 2;
+  const int nb = (int)(rows / FWDT_ROWS);
+  const size_t lds = FWDT_ROWS * (cols + 8) * 2;
   auto xp = (const bf16_t*)x;
   auto rp = (const bf16_t*)residual;
   auto wp = (const bf16_t*)weight;
