@@ -57,6 +57,9 @@ constexpr int QT = 32;   // dkv kernel: query rows per tile
 #ifndef PICO_KV_PIPE
 #define PICO_KV_PIPE 0
 #endif
+#ifndef PICO_KV_ROUND
+#define PICO_KV_ROUND 1
+#endif
 
 // PICO_BWDKV_STAMP: diagnostic build — workgroup 0 of the dK/dV kernel records s_memtime per (wave, tile,
 // phase) and writes them after the workspace (pico_attn_bwd_split_workspace grows by STAMP_BYTES)
@@ -87,9 +90,11 @@ struct KVCfg {
   static constexpr int QIMG = QT * RB;   // one Q (or dO) tile image
   static constexpr int LSD = 1024;       // LSE*log2e [32] | -delta [32] (one DMA piece)
   static constexpr int SLOT = 2 * QIMG + LSD;
+  // PICO_KV_ROUND: tiles per barrier interval (one wait + barrier + DMA issue serves R tiles);
   // PICO_KV_PIPE: the interval of tile t also reads slot t + 1 (S / dP of the next tile), so one more slot
-  static constexpr int PD = PICO_KV_PIPE ? 3 : 2;  // prefetch distance
-  static constexpr int NBUF = PD + 1;              // ring slots
+  static constexpr int R = PICO_KV_PIPE ? 1 : PICO_KV_ROUND;
+  static constexpr int PD = PICO_KV_PIPE ? 3 : 2 * R;   // prefetch distance (tiles): two intervals ahead
+  static constexpr int NBUF = PICO_KV_PIPE ? 4 : 3 * R;  // ring slots
   static constexpr int RPP = 1024 / RB;
   static constexpr int NQP = QIMG / 1024;
   static constexpr int NP = 2 * NQP + 1;
@@ -742,36 +747,46 @@ __global__ __launch_bounds__(KNW * 64, PICO_KV_MINB) void attn_bwd_kv_kernel(con
   }
 #else
   // Unrolled by the ring depth: the slot of every LDS read is a compile-time constant (immediate offsets).
+  // R tiles per barrier interval: one counted wait, one barrier and one DMA issue round serve R tiles.
   // (Measured and dropped, C2 causal: a stagger of the two waves of each SIMD by one phase — +2 %; carrying
   // S / dP of tile t + 1 across the barrier so M1(t + 1) overlaps V(t) inside the wave — +6 %.)
+  constexpr int R = C::R;
+  constexpr int NPMY_LO = C::NP / KNW;  // this wave's pieces per tile: NPMY_LO or NPMY_LO + 1
   int q0cur = q00;
   for (int t0 = 0; t0 < ntiles; t0 += C::NBUF) {
 #pragma unroll
-    for (int u = 0; u < C::NBUF; ++u) {
+    for (int u = 0; u < C::NBUF; u += R) {
       const int t = t0 + u;
       if (t >= ntiles) break;
       stamp(t, 0);
       if (t > 0) {
-        // this wave's pieces of tile t landed; tile t + 1's (issued one iteration later) may stay in flight
-        if (t + 1 < ntiles) {
-          if (wave < C::NP % KNW) wait_vmcnt(C::NP / KNW + 1);  // constant after inlining: one branch
-          else wait_vmcnt(C::NP / KNW);
+        // this wave's pieces of tiles t .. t + R - 1 landed; the next interval's R tiles may stay in flight
+        if (t + 2 * R <= ntiles) {
+          if (wave < C::NP % KNW) wait_vmcnt(R * (NPMY_LO + 1));
+          else wait_vmcnt(R * NPMY_LO);
         } else {
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
-        lds_barrier();  // everyone's pieces of tile t visible; slot (t + PD) % NBUF no longer read
+        lds_barrier();  // everyone's pieces visible; slots of tiles t - R .. t - 1 no longer read
       }
       stamp(t, 1);
-      if (t + PD < ntiles) issue((u + PD) % C::NBUF, nxt);
-      advance(nxt);
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        if (t + PD + i < ntiles) issue((u + PD + i) % C::NBUF, nxt);
+        advance(nxt);
+      }
       stamp(t, 2);
-      f32x16 s[KH], dp[KH];
-      bf16x8 pf[KH][2], sf[KH][2];
-      m1(u, q0cur, s, dp);
-      vsm(u, s, dp, pf, sf);
-      m2(u, pf, sf);
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        if (i > 0 && t + i >= ntiles) break;
+        f32x16 s[KH], dp[KH];
+        bf16x8 pf[KH][2], sf[KH][2];
+        m1(u + i, q0cur, s, dp);
+        vsm(u + i, s, dp, pf, sf);
+        m2(u + i, pf, sf);
+        q0cur = q0cur + QT >= qend ? qstart : q0cur + QT;
+      }
       stamp(t, 4);
-      q0cur = q0cur + QT >= qend ? qstart : q0cur + QT;
     }
   }
 
