@@ -168,7 +168,7 @@ template <int D, bool CAUSAL>
 __global__ __launch_bounds__(BwdCfg<D>::NTH, bwd_waves_per_eu<D>()) void attn_bwd_kernel(
     const pico_attn_args a, float scale, float scale_log2, const float* __restrict__ delta_g,
     const float* __restrict__ lse2_g, int sq_pad, float* __restrict__ dq_part, int64_t slab,
-    float* __restrict__ trash, int hsplit, float* __restrict__ dkv_part) {
+    float* __restrict__ trash, int hsplit, float* __restrict__ dkv_part, int kb0) {
   using C = BwdCfg<D>;
   constexpr int KS = C::KS, DT = C::DT, CPR = C::CPR, NW = C::NW;
   __shared__ __attribute__((aligned(16))) char smem[C::SMEM];
@@ -197,7 +197,7 @@ __global__ __launch_bounds__(BwdCfg<D>::NTH, bwd_waves_per_eu<D>()) void attn_bw
   // be split over `hsplit` workgroups (hs) so the grid fills the chip; each then writes fp32 dK/dV
   // partials that attn_bwd_dkv_kernel sums
   const int nbh = (int)(a.batch * a.heads_kv) * hsplit;
-  const int kb = blockIdx.x / nbh;
+  const int kb = kb0 + (int)(blockIdx.x / nbh);  // key block; slab kb - kb0 of this launch
   const int bhs = blockIdx.x % nbh;
   const int hs = bhs % hsplit;
   const int bh = bhs / hsplit;
@@ -502,7 +502,7 @@ __global__ __launch_bounds__(BwdCfg<D>::NTH, bwd_waves_per_eu<D>()) void attn_bw
       // every lane stores (rows past Sq go to a trash slot), so the per-tile count of vector-memory
       // instructions is fixed and the ring's vmcnt waits stay exact
       const int qr = c.q0 + qi * 16 + 4 * g16;  // this lane's first row
-      float* dst = dq_part + kb * slab + ((int64_t)b * Sq + qr) * Hq * D + c.hq * D + di * 16 + i16;
+      float* dst = dq_part + (kb - kb0) * slab + ((int64_t)b * Sq + qr) * Hq * D + c.hq * D + di * 16 + i16;
       const int rs = Hq * D;  // row stride (elements)
       if (c.q0 + BQ <= Sq) {  // wave-uniform: whole tile in range
 #pragma unroll
@@ -677,7 +677,7 @@ __global__ __launch_bounds__(BwdCfg<D>::NTH, bwd_waves_per_eu<D>()) void attn_bw
 // epilogue), rotated back in place.
 template <int D, bool CAUSAL>
 __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const pico_attn_args a, const float* __restrict__ dq_part,
-                                                          int64_t slab, int nkb, int f32acc, int rope_dk) {
+                                                          int64_t slab, int nkb, int f32acc, int rope_dk, int kb0) {
   constexpr int TPR = D / 16;  // threads per row
   const int64_t rows = a.batch * a.seqlen_q * a.heads_q;
   const int64_t row = ((int64_t)blockIdx.x * 256 + threadIdx.x) / TPR;
@@ -712,7 +712,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const pico_attn_args a
   const int64_t bq = row / a.heads_q;
   const int q = (int)(bq % a.seqlen_q);
   const int b = (int)(bq / a.seqlen_q);
-  const int last = CAUSAL ? min(nkb - 1, q / BK) : nkb - 1;
+  const int last = CAUSAL ? min(nkb - 1, q / BK - kb0) : nkb - 1;  // slabs k = key blocks kb0 + k
   float x1[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, x2[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   for (int k = 0; k <= last; ++k) {
     const f32x4* lo = reinterpret_cast<const f32x4*>(dq_part + k * slab + row * D + d0);
@@ -767,52 +767,86 @@ int64_t lsd_floats(const pico_attn_args* a) {
   return ((n + 63) / 64) * 64;
 }
 
+// Key blocks per launch of the fused kernel: its dQ partial slabs (one fp32 [B, Sq, Hq, D] per key block)
+// are bounded by this many; longer sequences run the key blocks in groups, each group's slab sum added
+// into an fp32 dQ (the slab workspace grew as S^2 / 256)
+#ifndef PICO_BWD_KB_CAP
+#define PICO_BWD_KB_CAP 8
+#endif
+int kb_groups(const pico_attn_args* a) {
+  const int64_t nkb = (a->seqlen_k + BK - 1) / BK;
+  return (int)((nkb + PICO_BWD_KB_CAP - 1) / PICO_BWD_KB_CAP);
+}
+
 template <int D>
 int launch_bwd(const pico_attn_args* a, hipStream_t s) {
   const int f32acc = (a->flags & PICO_ATTN_DQ_F32_ACCUM) != 0;
   const int sq_pad = sq_padded(a);
+  const int nkb = (int)((a->seqlen_k + BK - 1) / BK);
+  const int ngroups = kb_groups(a);
+  const int kbcap = ngroups > 1 ? PICO_BWD_KB_CAP : nkb;  // slabs held at once
   float* lse2 = (float*)a->workspace;
   float* delta = lse2 + lsd_floats(a);
   float* dq_part = delta + lsd_floats(a);
-  float* trash = dq_part + (int64_t)((a->seqlen_k + BK - 1) / BK) * a->batch * a->seqlen_q * a->heads_q * D;
   const int64_t slab = a->batch * a->seqlen_q * a->heads_q * D;
+  float* trash = dq_part + (int64_t)kbcap * slab;
+  // grouped: an fp32 dQ [B, Sq, Hq, D] after the slabs accumulates the groups (unless the caller's dQ is fp32)
+  float* dq32 = (ngroups > 1 && !f32acc) ? trash + 64 + STAMP_BYTES / 4 : nullptr;
   const int64_t rows = a->batch * a->seqlen_q * a->heads_q;
   // attn_bwd_dq_kernel: D/16 threads per row; with ROPE_BWD on the one-workgroup-per-key-block grid it
-  // also rotates the dK rows (the split grid's attn_bwd_dkv_kernel already did)
+  // also rotates the dK rows (the split grid's attn_bwd_dkv_kernel already did) — in the last group only
   const int rope_dk = (a->flags & PICO_ATTN_ROPE_BWD) && hsplit_for(a) == 1;
   const int64_t kv_rows = rope_dk ? a->batch * a->seqlen_k * a->heads_kv : 0;
-  const int row_blocks = pico_cdiv((rows + kv_rows) * (D / 16), 256);
   const int pre_blocks = pico_cdiv(a->batch * a->heads_q * (int64_t)sq_pad * (D / 8), 256);
   PICO_LAUNCH(PICO_K_ATTN_BWD_PRE, "attn_bwd_pre", s,
               attn_bwd_pre_kernel<D><<<pre_blocks, 256, 0, s>>>(*a, delta, lse2, sq_pad));
-  const int nkb = (int)((a->seqlen_k + BK - 1) / BK);
   const int hsplit = hsplit_for(a);
-  const int64_t nblk = (int64_t)nkb * a->batch * a->heads_kv * hsplit;
-  // fp32 dK/dV partials (hsplit > 1) after the trash slot and the diagnostic stamps
-  float* dkv_part = hsplit > 1 ? trash + 64 + STAMP_BYTES / 4 : nullptr;
+  // fp32 dK/dV partials (hsplit > 1) after the trash slot, the diagnostic stamps and dq32
+  float* dkv_part = hsplit > 1 ? trash + 64 + STAMP_BYTES / 4 + (dq32 ? slab : 0) : nullptr;
   const float sl2 = a->softmax_scale * LOG2E;
-  if (nblk > 0) {
-    if (a->causal) {
-      PICO_LAUNCH(PICO_K_ATTN_BWD, "attn_bwd", s,
-                  attn_bwd_kernel<D, true><<<(int)nblk, BwdCfg<D>::NTH, 0, s>>>(
-                      *a, a->softmax_scale, sl2, delta, lse2, sq_pad, dq_part, slab, trash, hsplit, dkv_part));
-    } else {
-      PICO_LAUNCH(PICO_K_ATTN_BWD, "attn_bwd", s,
-                  attn_bwd_kernel<D, false><<<(int)nblk, BwdCfg<D>::NTH, 0, s>>>(
-                      *a, a->softmax_scale, sl2, delta, lse2, sq_pad, dq_part, slab, trash, hsplit, dkv_part));
+  pico_attn_args ag = *a;  // the dQ-sum launches' view: grouped -> fp32 accumulate into dq32
+  if (dq32) {
+    if (hipMemsetAsync(dq32, 0, (size_t)slab * 4, s) != hipSuccess) return pico_set_error("pico_attn_bwd: memset failed");
+    ag.dq = dq32;
+    ag.dq_strides[0] = a->seqlen_q * a->heads_q * D;
+    ag.dq_strides[1] = a->heads_q * D;
+    ag.dq_strides[2] = D;
+  }
+  const int acc = (f32acc || dq32) ? 1 : 0;
+  for (int g = 0; g < ngroups; ++g) {
+    const int kb0 = g * kbcap, n = min(kbcap, nkb - kb0);
+    const int64_t nblk = (int64_t)n * a->batch * a->heads_kv * hsplit;
+    if (nblk > 0) {
+      if (a->causal) {
+        PICO_LAUNCH(PICO_K_ATTN_BWD, "attn_bwd", s,
+                    attn_bwd_kernel<D, true><<<(int)nblk, BwdCfg<D>::NTH, 0, s>>>(
+                        *a, a->softmax_scale, sl2, delta, lse2, sq_pad, dq_part, slab, trash, hsplit, dkv_part, kb0));
+      } else {
+        PICO_LAUNCH(PICO_K_ATTN_BWD, "attn_bwd", s,
+                    attn_bwd_kernel<D, false><<<(int)nblk, BwdCfg<D>::NTH, 0, s>>>(
+                        *a, a->softmax_scale, sl2, delta, lse2, sq_pad, dq_part, slab, trash, hsplit, dkv_part, kb0));
+      }
     }
-    if (hsplit > 1) {
-      const int kv_blocks = pico_cdiv(a->batch * a->seqlen_k * a->heads_kv * (D / 16), 256);
-      PICO_LAUNCH(PICO_K_ATTN_BWD_DKV, "attn_bwd_dkv", s,
-                  attn_bwd_dkv_kernel<D><<<kv_blocks, 256, 0, s>>>(*a, dkv_part, hsplit));
+    const int rdk = (g == ngroups - 1) ? rope_dk : 0;
+    const int row_blocks = pico_cdiv((rows + (rdk ? kv_rows : 0)) * (D / 16), 256);
+    if (a->causal) {
+      PICO_LAUNCH(PICO_K_ATTN_BWD_DQ, "attn_bwd_dq", s,
+                  attn_bwd_dq_kernel<D, true><<<row_blocks, 256, 0, s>>>(ag, dq_part, slab, n, acc, rdk, kb0));
+    } else {
+      PICO_LAUNCH(PICO_K_ATTN_BWD_DQ, "attn_bwd_dq", s,
+                  attn_bwd_dq_kernel<D, false><<<row_blocks, 256, 0, s>>>(ag, dq_part, slab, n, acc, rdk, kb0));
     }
   }
-  if (a->causal) {
+  if (hsplit > 1 && nkb > 0) {
+    const int kv_blocks = pico_cdiv(a->batch * a->seqlen_k * a->heads_kv * (D / 16), 256);
+    PICO_LAUNCH(PICO_K_ATTN_BWD_DKV, "attn_bwd_dkv", s, attn_bwd_dkv_kernel<D><<<kv_blocks, 256, 0, s>>>(*a, dkv_part, hsplit));
+  }
+  if (dq32) {  // dq32 (RoPE^-1 already applied per group: the rotation is linear) -> the caller's bf16 dQ
+    pico_attn_args ac = *a;
+    ac.flags = 0;
+    const int row_blocks = pico_cdiv(rows * (D / 16), 256);
     PICO_LAUNCH(PICO_K_ATTN_BWD_DQ, "attn_bwd_dq", s,
-                attn_bwd_dq_kernel<D, true><<<row_blocks, 256, 0, s>>>(*a, dq_part, slab, nkb, f32acc, rope_dk));
-  } else {
-    PICO_LAUNCH(PICO_K_ATTN_BWD_DQ, "attn_bwd_dq", s,
-                attn_bwd_dq_kernel<D, false><<<row_blocks, 256, 0, s>>>(*a, dq_part, slab, nkb, f32acc, rope_dk));
+                attn_bwd_dq_kernel<D, false><<<row_blocks, 256, 0, s>>>(ac, dq32, slab, 1, 0, 0, 0));
   }
   return 0;
 }
@@ -852,12 +886,16 @@ int64_t pico_attn_args_size(void) { return (int64_t)sizeof(pico_attn_args); }
 
 int64_t pico_attn_bwd_workspace_bytes(const pico_attn_args* a) {
   if (PICO_BWD_SPLIT_D64 && a->head_dim == 64) return pico_attn_bwd_split_workspace(a);
-  // lse2, delta [B*Hq*Sq_pad] fp32 + one fp32 dQ partial slab [B, Sq, Hq, D] per 256-key block
+  // lse2, delta [B*Hq*Sq_pad] fp32 + one fp32 dQ partial slab [B, Sq, Hq, D] per 256-key block of a group
+  // (at most PICO_BWD_KB_CAP; grouped: + an fp32 dQ accumulator unless the caller's dQ is fp32)
   const int64_t nkb = (a->seqlen_k + BK - 1) / BK;
+  const int ng = kb_groups(a);
+  const int64_t slab = a->batch * a->seqlen_q * a->heads_q * a->head_dim;
+  const int64_t nslab = (ng > 1 ? PICO_BWD_KB_CAP : nkb) + ((ng > 1 && !(a->flags & PICO_ATTN_DQ_F32_ACCUM)) ? 1 : 0);
   // + 64 floats of trash for the dQ stores of padded query rows
   const int hs = hsplit_for(a);
   const int64_t dkv = hs > 1 ? 2 * hs * a->batch * a->seqlen_k * a->heads_kv * a->head_dim : 0;  // fp32 partials
-  return (2 * lsd_floats(a) + nkb * a->batch * a->seqlen_q * a->heads_q * a->head_dim + 64 + dkv) * 4 + STAMP_BYTES;
+  return (2 * lsd_floats(a) + nslab * slab + 64 + dkv) * 4 + STAMP_BYTES;
 }
 
 int pico_attn_bwd(const pico_attn_args* a, void* stream) {

@@ -85,6 +85,10 @@ def test_workspace_sizes(lib):
     a.batch, a.seqlen_q, a.seqlen_k, a.heads_q, a.heads_kv, a.head_dim = 2, 1024, 1024, 16, 16, 128
     assert lib.pico_attn_bwd_workspace_bytes(ctypes.byref(a)) == 2 * 2 * 16 * 1024 * 4 + 4 * (2 * 1024 * 16 * 128 * 4) + 256 \
         + 2 * 4 * 2 * 1024 * 16 * 128 * 4  # B 2 x 16 heads x 4 key blocks = 128 workgroups: dK/dV split 4 ways
+    # head_dim 128 past 8 key blocks: slabs bounded at 8 (+ an fp32 dQ accumulator), not one per block
+    a.batch, a.seqlen_q, a.seqlen_k, a.heads_q, a.heads_kv = 1, 16384, 16384, 32, 32
+    slab = 16384 * 32 * 128 * 4
+    assert lib.pico_attn_bwd_workspace_bytes(ctypes.byref(a)) == 2 * 32 * 16384 * 4 + (8 + 1) * slab + 256
 
 
 def test_ops_fail_loudly_without_hip_tensors(lib):

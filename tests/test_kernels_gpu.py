@@ -8,6 +8,7 @@ Tolerances (bf16 outputs vs an fp64/fp32 oracle on the SAME bf16 inputs):
   * LSE (fp32): max-abs <= 2e-3;
   * DP bucket kernels: bit-exact.
 """
+import ctypes
 import math
 
 import pytest
@@ -275,6 +276,54 @@ def test_attention_gqa_head_split(B, Hq, Hkv):
     assert rel_l2(dq.transpose(1, 2).float(), gq) < 1e-2
     assert rel_l2(dk.transpose(1, 2).float(), gk) < 1e-2
     assert rel_l2(dv.transpose(1, 2).float(), gv) < 1e-2
+
+
+@pytest.mark.parametrize("S,Hq,Hkv,causal,mode", [(2300, 2, 2, True, "bf16"), (2304, 4, 2, False, "bf16"),
+                                                   (2300, 2, 1, True, "f32acc"), (2304, 2, 2, True, "rope"),
+                                                   (2304, 64, 64, True, "rope")])  # one workgroup per key block: dK RoPE^-1 in the last group
+def test_attention_bwd_d128_key_block_groups(S, Hq, Hkv, causal, mode):
+    """head_dim 128 past PICO_BWD_KB_CAP (8) key blocks: the fused backward runs its key blocks in groups with a
+    bounded number of dQ slabs, the groups' sums added into an fp32 dQ. vs an fp32 torch
+    reference: bf16 dQ, the caller's fp32 accumulator (ring mode), and the fused RoPE^-1 (rotation per
+    group, dK rotated once after the last)."""
+    from picotron_amd.model import get_cos_sin
+    ops = _ops()
+    torch.manual_seed(S + Hq + Hkv)
+    B, D = 1, 128
+    q, do = [torch.randn(B, S, Hq, D, dtype=BF, device=DEV) for _ in range(2)]
+    k, v = [torch.randn(B, S, Hkv, D, dtype=BF, device=DEV) for _ in range(2)]
+    sc = 1.0 / math.sqrt(D)
+    o, lse = ops.attention_block_fwd(q, k, v, sc, causal)
+    assert -(-S // 256) > 8  # grouped (the bound itself: tests/test_abi.py::test_workspace_sizes)
+    G = Hq // Hkv
+    qf, kf, vf = [t.float().transpose(1, 2).requires_grad_(True) for t in (q, k, v)]
+    kr, vr = kf.repeat_interleave(G, 1), vf.repeat_interleave(G, 1)
+    sm = (qf @ kr.transpose(-1, -2)) * sc
+    if causal:
+        sm = sm.masked_fill(torch.triu(torch.ones(S, S, dtype=torch.bool, device=DEV), 1), float("-inf"))
+    out = torch.softmax(sm, -1) @ vr
+    gq, gk, gv = torch.autograd.grad(out, (qf, kf, vf), do.float().transpose(1, 2))
+    gq, gk, gv = (t.transpose(1, 2) for t in (gq, gk, gv))
+    if mode == "bf16":
+        dq, dk, dv = ops.attention_block_bwd(do, q, k, v, o, lse, sc, causal)
+        dq = dq.float()
+    elif mode == "f32acc":
+        dq = torch.full(q.shape, 0.25, dtype=torch.float32, device=DEV)
+        _, dk, dv = ops.attention_block_bwd(do, q, k, v, o, lse, sc, causal, dq_accum=dq)
+        dq = dq - 0.25
+    else:
+        cos, sin = get_cos_sin(S, D, base=10000.0)
+        cos, sin = cos.to(DEV, BF)[:, : D // 2], sin.to(DEV, BF)[:, : D // 2]
+        dq, dk, dv = [torch.empty_like(t) for t in (q, k, v)]
+        ops._attention_bwd_into(do, q, k, v, o, lse, sc, causal, dq, dk, dv, rope=(cos, sin))
+        rq, rk = torch.empty_like(q), torch.empty_like(k)
+        ops._rope_launch(gq.to(BF).contiguous(), rq, cos, sin, True)
+        ops._rope_launch(gk.to(BF).contiguous(), rk, cos, sin, True)
+        gq, gk = rq.float(), rk.float()
+        dq = dq.float()
+    assert rel_l2(dq, gq) < 1e-2
+    assert rel_l2(dk.float(), gk) < 1e-2
+    assert rel_l2(dv.float(), gv) < 1e-2
 
 
 def test_attention_dq_f32_accumulate():
