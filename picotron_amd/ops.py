@@ -17,6 +17,7 @@ Extra entry points used by picotron_amd's own modules:
 import ctypes
 import math
 import os
+import weakref
 
 import torch
 from torch.optim.optimizer import register_optimizer_step_post_hook as _register_step_post_hook
@@ -335,9 +336,14 @@ def wgrad_accumulate(params, dy2, x2):
 # parameters' version counters) or an in-place write that bumps a version counter.
 # refresh_weight_transposes() brings every cached copy up to date eagerly; MicroBatchGraph calls it
 # before each replay (a replayed graph runs no host code, so it could not notice stale copies).
+# Writes that bump neither counter — through `p.data` (p.data.copy_(), a checkpoint load into .data),
+# or by an optimizer that is not a torch.optim.Optimizer — must be followed by
+# invalidate_weight_transposes(). Entries are keyed by the weight's storage (identity and data pointer)
+# and shape, and hold the parameters W is made of only through weak references: a rebuilt model does
+# not keep the old one's weights alive, and entries whose parameters died are dropped.
 # --------------------------------------------------------------------------------------------
 _WT_GEN = [0]
-_WT_CACHE = {}  # W.data_ptr() -> [wt, key, W, params]
+_WT_CACHE = {}  # (storage id, W.data_ptr(), shape) -> [wt, key, [weakref(p) for p in params]]
 _WT_HOOK = []
 
 
@@ -345,9 +351,24 @@ def _bump_wt_gen(*_):
     _WT_GEN[0] += 1
 
 
+def invalidate_weight_transposes():
+    """Mark every cached W^T stale (re-transposed on next use): call after writing weights through
+    `.data` or with a non-torch.optim optimizer."""
+    _bump_wt_gen()
+
+
 def wt_dgrad_enabled():
     """PICO_WT_DGRAD=0 computes dgrads as dy @ W (no transposed copies)."""
     return os.getenv("PICO_WT_DGRAD", "1") != "0"
+
+
+def _wt_key(W):
+    return (W.untyped_storage()._cdata, W.data_ptr(), tuple(W.shape))
+
+
+def _wt_purge():
+    for k in [k for k, e in _WT_CACHE.items() if any(r() is None for r in e[2])]:
+        del _WT_CACHE[k]
 
 
 def weight_t(W, params):
@@ -355,10 +376,14 @@ def weight_t(W, params):
     if not _WT_HOOK:
         _WT_HOOK.append(_register_step_post_hook(_bump_wt_gen))
     key = (_WT_GEN[0],) + tuple(p._version for p in params)
-    ent = _WT_CACHE.get(W.data_ptr())
-    if ent is None or tuple(ent[0].shape) != (W.shape[1], W.shape[0]) or ent[0].dtype != W.dtype:
-        ent = [torch.empty((W.shape[1], W.shape[0]), dtype=W.dtype, device=W.device), None, W, params]
-        _WT_CACHE[W.data_ptr()] = ent
+    ck = _wt_key(W)
+    ent = _WT_CACHE.get(ck)
+    if (ent is None or ent[0].dtype != W.dtype or len(ent[2]) != len(params)
+            or any(r() is not p for r, p in zip(ent[2], params))):
+        _wt_purge()
+        ent = [torch.empty((W.shape[1], W.shape[0]), dtype=W.dtype, device=W.device), None,
+               [weakref.ref(p) for p in params]]
+        _WT_CACHE[ck] = ent
     if ent[1] != key:
         with torch.no_grad():
             transpose_2d(W, out=ent[0])
@@ -398,8 +423,11 @@ def _wgrad_input(x2, n_out, x=None):
 
 
 def refresh_weight_transposes():
+    _wt_purge()
     for ent in list(_WT_CACHE.values()):
-        weight_t(ent[2], ent[3])
+        params = [r() for r in ent[2]]
+        W = params[0].detach() if len(params) == 1 else stacked_weight(params)
+        weight_t(W, params)
 
 
 def dgrad(dy2, W, params):

@@ -104,3 +104,28 @@ def test_ops_fail_loudly_without_hip_tensors(lib):
         ops.flash_attn_func(x, x, x, dropout_p=0.1)
     with pytest.raises(NotImplementedError):
         ops.layer_norm_fn(x, None, None, is_rms_norm=False)
+
+
+def test_weight_transpose_cache_host_logic(monkeypatch):
+    """ops.weight_t's cache: one entry per weight storage, reused across the fresh stacked
+    views each call builds; invalidate_weight_transposes() after a .data write (no version bump) makes the
+    next use re-transpose; entries hold their parameters only weakly and die with them. (CPU tensors: the
+    transpose falls back to a strided copy; the cache logic is the same.)"""
+    import gc
+    from picotron_amd import ops
+    monkeypatch.setattr(ops, "_WT_CACHE", {})
+    monkeypatch.setattr(ops, "_WT_HOOK", [None])
+    a = torch.nn.Parameter(torch.randn(8, 16))
+    b = torch.nn.Parameter(torch.randn(8, 16))
+    t1 = ops.weight_t(ops.stacked_weight((a, b)), (a, b))
+    assert torch.equal(t1, torch.cat([a, b]).t())
+    assert ops.weight_t(ops.stacked_weight((a, b)), (a, b)) is t1 and len(ops._WT_CACHE) == 1
+    with torch.no_grad():
+        a.data.mul_(2)  # bumps no version counter the cache sees
+    assert not torch.equal(ops.weight_t(ops.stacked_weight((a, b)), (a, b)), torch.cat([a, b]).t())
+    ops.invalidate_weight_transposes()
+    assert torch.equal(ops.weight_t(ops.stacked_weight((a, b)), (a, b)), torch.cat([a, b]).t())
+    del a, b, t1
+    gc.collect()
+    ops._wt_purge()
+    assert len(ops._WT_CACHE) == 0
