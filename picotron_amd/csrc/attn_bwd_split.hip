@@ -67,7 +67,12 @@ constexpr int QT = 32;   // dkv kernel: query rows per tile
 #define PICO_BWDKV_STAMP 0
 #endif
 constexpr int STAMP_T = 48, STAMP_P = 5;
-constexpr int64_t STAMP_BYTES = PICO_BWDKV_STAMP ? 8 * STAMP_T * STAMP_P * 8 : 0;
+// PICO_BWDKV_WGSTAMP: diagnostic build — every dK/dV workgroup records s_memrealtime (100 MHz, chip-wide)
+// at entry, loop start, loop end and after its stores drained (4 x 8 B per workgroup, grids <= 65536)
+#ifndef PICO_BWDKV_WGSTAMP
+#define PICO_BWDKV_WGSTAMP 0
+#endif
+constexpr int64_t STAMP_BYTES = PICO_BWDKV_STAMP ? 8 * STAMP_T * STAMP_P * 8 : (PICO_BWDKV_WGSTAMP ? 65536 * 4 * 8 : 0);
 
 #ifndef PICO_BWDQ_NBUF
 #define PICO_BWDQ_NBUF 3
@@ -392,6 +397,10 @@ __global__ __launch_bounds__(KNW * 64, PICO_KV_MINB) void attn_bwd_kv_kernel(con
   const int Sq = (int)a.seqlen_q, Sk = (int)a.seqlen_k;
   const int Hq = (int)a.heads_q;
   const int G = (int)(a.heads_q / a.heads_kv);
+#if PICO_BWDKV_WGSTAMP
+  unsigned long long wgs[4];
+  wgs[0] = __builtin_amdgcn_s_memrealtime();
+#endif
 
   // heaviest key blocks first (causal: block 0 sees every query); small grids split a key block's
   // (query head, query tile) list over `hsplit` workgroups with fp32 partials (attn_bwd_dkv_kernel sums)
@@ -541,6 +550,10 @@ __global__ __launch_bounds__(KNW * 64, PICO_KV_MINB) void attn_bwd_kv_kernel(con
   const bool kpad = kw + KPW - 1 >= Sk;  // wave-uniform: some of the wave's keys are padding
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();  // prologue tiles visible
+#if PICO_BWDKV_WGSTAMP
+  wgs[1] = __builtin_amdgcn_s_memrealtime();
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+#endif
 
 #if PICO_BWDKV_STAMP
   __shared__ unsigned long long stamps[KNW * STAMP_T * STAMP_P];
@@ -795,6 +808,9 @@ __global__ __launch_bounds__(KNW * 64, PICO_KV_MINB) void attn_bwd_kv_kernel(con
   if (blockIdx.x == 0)
     for (int i = lane; i < STAMP_T * STAMP_P; i += 64) stamp_out[wave * STAMP_T * STAMP_P + i] = stamps[wave * STAMP_T * STAMP_P + i];
 #endif
+#if PICO_BWDKV_WGSTAMP
+  wgs[2] = __builtin_amdgcn_s_memrealtime();
+#endif
   // ---- epilogue: lane = key kw + 32 kt + r, register i of tile dt = d 32 dt + acc_row(i, h) ----
   if (hsplit == 1) {
     const bool rope = (a.flags & PICO_ATTN_ROPE_BWD) != 0;
@@ -849,6 +865,12 @@ __global__ __launch_bounds__(KNW * 64, PICO_KV_MINB) void attn_bwd_kv_kernel(con
         }
     }
   }
+#if PICO_BWDKV_WGSTAMP
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  wgs[3] = __builtin_amdgcn_s_memrealtime();
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  if (wave == 0 && lane < 4 && blockIdx.x < 65536) stamp_out[blockIdx.x * 4 + lane] = wgs[lane & 3];
+#endif
 }
 
 int split_sq_pad(const pico_attn_args* a) { return (int)((a->seqlen_q + QT - 1) / QT) * QT; }
