@@ -77,6 +77,12 @@ constexpr int64_t STAMP_BYTES = PICO_BWDKV_STAMP ? 8 * STAMP_T * STAMP_P * 8 : (
 #ifndef PICO_BWDQ_NBUF
 #define PICO_BWDQ_NBUF 3
 #endif
+#ifndef PICO_BWDQ_MINB
+#define PICO_BWDQ_MINB 3  // dQ kernel workgroups per CU the register budget is sized for (168 VGPRs)
+#endif
+#ifndef PICO_BWDQ_SPLITKT
+#define PICO_BWDQ_SPLITKT 1  // A/B C2 (us): 45.7 -> 44.1 with MINB 3; S 4096: 115.9 -> 107.4
+#endif
 
 template <int D>
 struct QCfg {
@@ -137,7 +143,7 @@ PICO_DEV void tr_offsets(int lane, unsigned (&tro)[D / 32][2]) {
 // dQ kernel (query-major)
 // ------------------------------------------------------------------------------------------------
 template <int D, bool CAUSAL>
-__global__ __launch_bounds__(256, 2) void attn_bwd_q_kernel(const pico_attn_args a, float scale, float scale_log2,
+__global__ __launch_bounds__(256, PICO_BWDQ_MINB) void attn_bwd_q_kernel(const pico_attn_args a, float scale, float scale_log2,
                                                              float* __restrict__ lse2_g, float* __restrict__ delta_g,
                                                              int sq_pad) {
   using C = QCfg<D>;
@@ -263,6 +269,47 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_q_kernel(const pico_attn_args
   // One 64-key tile: S^T, dP^T (8 + 8 MFMAs), P^T and dS^T in registers, dQ^T += K^T dS^T (8 MFMAs).
   // kb: the slot's K image (V image at +IMG). One body for every tile (the causal / padding mask is an
   // in-place branch on S), so the loop-carried dQ accumulators never move between registers.
+#if PICO_BWDQ_SPLITKT
+  // the two 32-key halves of a tile one after the other (half the K / V fragments and S / dP registers
+  // live at a time: room for a third workgroup per CU, PICO_BWDQ_MINB)
+  auto tile = [&](const char* kb, bool mask, int n0) __attribute__((always_inline)) {
+    const char* vb = kb + C::IMG;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      bf16x8 kf[KS], vf[KS];
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        kf[ks] = lds_read_b128(kb, ro[ks] + kt * 32 * RB);
+        vf[ks] = lds_read_b128(vb, ro[ks] + kt * 32 * RB);
+      }
+      f32x16 sc, dpc;
+      if (mask) {
+        const int rel = lim_lane - n0 - 4 * h;
+        f32x16 m;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) m[i] = (32 * kt + (i & 3) + 8 * (i >> 2)) <= rel ? 0.f : -INFINITY;
+        sc = mfma32(kf[0], qf[0], m);
+      } else {
+        sc = mfma32(kf[0], qf[0], (f32x16)0.f);
+      }
+#pragma unroll
+      for (int ks = 1; ks < KS; ++ks) sc = mfma32(kf[ks], qf[ks], sc);
+      dpc = mfma32(vf[0], df[0], ndelta);
+#pragma unroll
+      for (int ks = 1; ks < KS; ++ks) dpc = mfma32(vf[ks], df[ks], dpc);
+      float ds[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) ds[i] = fast_exp2(__builtin_fmaf(sc[i], scale_log2, nl2)) * dpc[i];
+      const bf16x8 dsf[2] = {pack_bf16x8(ds), pack_bf16x8(ds + 8)};
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        const char* rowb = kb + (32 * kt + 16 * st) * RB;
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) dq[dt] = mfma32(tr_pair(rowb, tro[dt][0], tro[dt][1]), dsf[st], dq[dt]);
+      }
+    }
+  };
+#else
   auto tile = [&](const char* kb, bool mask, int n0) __attribute__((always_inline)) {
     const char* vb = kb + C::IMG;
     bf16x8 kf[2][KS], vf[2][KS];
@@ -317,6 +364,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_q_kernel(const pico_attn_args
       }
   };
 
+#endif
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // prologue tiles and loads landed
   // unrolled by the ring depth: every LDS read of a tile has a compile-time slot (immediate offsets)
   for (int t0 = 0; t0 < ntiles; t0 += C::NBUF) {
