@@ -43,8 +43,13 @@ constexpr int KT = 64;   // dq kernel: keys per tile
 #ifndef PICO_KV_KVB
 #define PICO_KV_KVB 128
 #endif
+// Workgroups per CU the register budget is sized for (a template parameter, chosen per launch by kv_minb):
+// 3 (168 VGPRs) for causal grids, whose LPT-ordered uneven blocks fill any number of slots: C2 58.5 -> 52.6
+// us, S 4096 153 -> 143; 2 (256 VGPRs) for non-causal grids, whose equal blocks would leave a third round
+// partly empty (C2 full: 1024 blocks = 2 rounds of 512 slots vs 1.33 rounds of 768) and whose body spills
+// at 168 VGPRs (83 vs 123 us).
 #ifndef PICO_KV_MINB
-#define PICO_KV_MINB 2
+#define PICO_KV_MINB 0  // 0: per launch (kv_minb); 2 or 3: forced
 #endif
 constexpr int KVB = PICO_KV_KVB;  // dkv kernel: keys per workgroup
 // dkv kernel: keys per wave. 64: 4 waves, one per SIMD, 2 key halves each (each Q/dO tile read serves 64
@@ -54,6 +59,9 @@ constexpr int KVB = PICO_KV_KVB;  // dkv kernel: keys per workgroup
 #endif
 constexpr int KPW = PICO_KV_KPW, KH = KPW / 32, KNW = KVB / KPW;
 constexpr int QT = 32;   // dkv kernel: query rows per tile
+#ifndef PICO_KV_SEQM1
+#define PICO_KV_SEQM1 1  // read dO's fragments after the S chain (-16 live VGPRs; C2 58.5 -> 56.1 us at MINB 2)
+#endif
 #ifndef PICO_KV_PIPE
 #define PICO_KV_PIPE 0
 #endif
@@ -429,8 +437,8 @@ __global__ __launch_bounds__(256, PICO_BWDQ_MINB) void attn_bwd_q_kernel(const p
 // ------------------------------------------------------------------------------------------------
 // dK / dV kernel (key-major)
 // ------------------------------------------------------------------------------------------------
-template <int D, bool CAUSAL>
-__global__ __launch_bounds__(KNW * 64, PICO_KV_MINB) void attn_bwd_kv_kernel(const pico_attn_args a, float scale, float scale_log2,
+template <int D, bool CAUSAL, int MINB>
+__global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kv_kernel(const pico_attn_args a, float scale, float scale_log2,
                                                               const float* __restrict__ lse2_g,
                                                               const float* __restrict__ delta_g, int sq_pad,
                                                               int hsplit, float* __restrict__ dkv_part,
@@ -626,7 +634,7 @@ __global__ __launch_bounds__(KNW * 64, PICO_KV_MINB) void attn_bwd_kv_kernel(con
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       qa[ks] = lds_read_b128(qs, qo[ks]);
-      da[ks] = lds_read_b128(dos, qo[ks]);
+      if (!PICO_KV_SEQM1) da[ks] = lds_read_b128(dos, qo[ks]);
     }
     f32x16 nd;  // rows of this lane's accumulator registers: q = q0 + 8 g + 4 h + (0..3)
 #pragma unroll
@@ -652,6 +660,22 @@ __global__ __launch_bounds__(KNW * 64, PICO_KV_MINB) void attn_bwd_kv_kernel(con
 #pragma unroll
       for (int kt = 0; kt < KH; ++kt) s[kt] = mfma32(qa[0], kf[kt][0], (f32x16)0.f);
     }
+#if PICO_KV_SEQM1
+    // the dO fragments are read once the S chain has consumed Q's (16 fewer live VGPRs: room for MINB 3)
+#pragma unroll
+    for (int kt = 0; kt < KH; ++kt)
+#pragma unroll
+      for (int ks = 1; ks < KS; ++ks) s[kt] = mfma32(qa[ks], kf[kt][ks], s[kt]);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) da[ks] = lds_read_b128(dos, qo[ks]);
+#pragma unroll
+    for (int kt = 0; kt < KH; ++kt) {
+      dp[kt] = mfma32(da[0], vf[kt][0], nd);
+#pragma unroll
+      for (int ks = 1; ks < KS; ++ks) dp[kt] = mfma32(da[ks], vf[kt][ks], dp[kt]);
+    }
+#else
 #pragma unroll
     for (int kt = 0; kt < KH; ++kt) {
 #pragma unroll
@@ -660,6 +684,7 @@ __global__ __launch_bounds__(KNW * 64, PICO_KV_MINB) void attn_bwd_kv_kernel(con
 #pragma unroll
       for (int ks = 1; ks < KS; ++ks) dp[kt] = mfma32(da[ks], vf[kt][ks], dp[kt]);
     }
+#endif
   };
   // V: P = exp2(S scale log2e - LSE log2e), dS = P dP, packed to bf16 (the B operands of M2)
   auto vsm = [&](int si, const f32x16 (&s)[KH], const f32x16 (&dp)[KH], bf16x8 (&pf)[KH][2], bf16x8 (&sf)[KH][2])
@@ -928,14 +953,22 @@ int64_t split_lsd_floats(const pico_attn_args* a) {
   return ((n + 63) / 64) * 64;
 }
 
-// split of a key block's tile list so that the dK/dV grid fills the 256 CUs (PICO_KV_MINB workgroups each)
+// dK/dV workgroups per CU (see PICO_KV_MINB): 3 for causal grids, 2 for non-causal ones (whose mask-free
+// body does not fit 168 VGPRs without spills either)
+int kv_minb(const pico_attn_args* a) {
+  if (PICO_KV_MINB) return PICO_KV_MINB;
+  return a->causal ? 3 : 2;
+}
+
+// split of a key block's tile list so that the dK/dV grid fills the 256 CUs (kv_minb workgroups each; GQA-4
+// C2 at MINB 3: kv + dkv 55.5 + 13.8 us with 4 parts, 67.2 + 9.6 with 2, 62.1 + 9.7 at MINB 2)
 int kv_hsplit(const pico_attn_args* a) {
   if (a->heads_kv <= 0 || a->heads_q % a->heads_kv != 0) return 1;
   const int64_t nblk = ((a->seqlen_k + KVB - 1) / KVB) * a->batch * a->heads_kv;
   const int64_t tiles = (a->heads_q / a->heads_kv) * ((a->seqlen_q + QT - 1) / QT);
   if (nblk <= 0) return 1;
   int d = 1;
-  while (d < 8 && nblk * d < 256 * PICO_KV_MINB && 2 * d <= tiles) d *= 2;
+  while (d < 8 && nblk * d < 256 * kv_minb(a) && 2 * d <= tiles) d *= 2;
   return d;
 }
 
@@ -960,10 +993,16 @@ int launch_split(const pico_attn_args* a, hipStream_t s) {
   const int hsplit = kv_hsplit(a);
   const int64_t nblk = (int64_t)nkb * a->batch * a->heads_kv * hsplit;
   if (nblk == 0) return 0;
-  PICO_LAUNCH(PICO_K_ATTN_BWD_KV, "attn_bwd_kv", s,
-              attn_bwd_kv_kernel<D, CAUSAL><<<(int)nblk, KNW * 64, 0, s>>>(
-                  *a, a->softmax_scale, sl2, lse2, delta, sq_pad, hsplit, dkv_part,
-                  (unsigned long long*)((char*)a->workspace + pico_attn_bwd_split_workspace(a) - STAMP_BYTES)));
+  unsigned long long* stamps = (unsigned long long*)((char*)a->workspace + pico_attn_bwd_split_workspace(a) - STAMP_BYTES);
+  if (CAUSAL && kv_minb(a) == 3) {
+    PICO_LAUNCH(PICO_K_ATTN_BWD_KV, "attn_bwd_kv", s,
+                attn_bwd_kv_kernel<D, CAUSAL, 3><<<(int)nblk, KNW * 64, 0, s>>>(
+                    *a, a->softmax_scale, sl2, lse2, delta, sq_pad, hsplit, dkv_part, stamps));
+  } else {
+    PICO_LAUNCH(PICO_K_ATTN_BWD_KV, "attn_bwd_kv", s,
+                attn_bwd_kv_kernel<D, CAUSAL, 2><<<(int)nblk, KNW * 64, 0, s>>>(
+                    *a, a->softmax_scale, sl2, lse2, delta, sq_pad, hsplit, dkv_part, stamps));
+  }
   if (hsplit > 1) {
     const int kv_blocks = pico_cdiv(a->batch * a->seqlen_k * a->heads_kv * (D / 16), 256);
     PICO_LAUNCH(PICO_K_ATTN_BWD_DKV, "attn_bwd_dkv", s,
