@@ -39,6 +39,9 @@
 #ifndef PICO_FWD_EARLY_V
 #define PICO_FWD_EARLY_V -1
 #endif
+// (Measured and dropped: the row sums out of the matrix pipe -- one v_mfma_f32_16x16x32_bf16 of a 0/1
+// operand with the packed P^T per 16-key half instead of 32 v_add_f32 per tile -- +2..4 % at D = 64; the
+// mask as the C operand of the first S MFMA -- spills at 128 VGPRs.)
 
 //   PICO_FWD_NBUF_D64 / PICO_FWD_WPE_D64: ring slots and waves per SIMD for D = 64. 2 / 4 (shipped):
 //     four 32-KiB workgroups per CU, prefetch distance 1, 128 VGPRs without spills; 3 / 3: three
