@@ -41,11 +41,28 @@
 #endif
 // (Measured and dropped: the row sums out of the matrix pipe -- one v_mfma_f32_16x16x32_bf16 of a 0/1
 // operand with the packed P^T per 16-key half instead of 32 v_add_f32 per tile -- +2..4 % at D = 64; the
-// mask as the C operand of the first S MFMA -- spills at 128 VGPRs.)
+// mask as the C operand of the first S MFMA -- spills at 128 VGPRs; no row max on the common path (P against
+// the running max, accepted when every lane's partial sum stays <= 2^THR, else S recomputed max-first) --
+// +16 % at C2 although the fallback never ran: the retry loop costs the compiler's schedule more than the 16
+// max3 it removes.)
 
 //   PICO_FWD_NBUF_D64 / PICO_FWD_WPE_D64: ring slots and waves per SIMD for D = 64. 2 / 4 (shipped):
 //     four 32-KiB workgroups per CU, prefetch distance 1, 128 VGPRs without spills; 3 / 3: three
 //     48-KiB workgroups per CU. Measured C2 causal 36.0 -> 34.8 us, full 54.9 -> 52.5, GQA 33.5 -> 32.3.
+// PICO_FWD_WGSTAMP: diagnostic build -- every workgroup records s_memrealtime (100 MHz, chip-wide) at entry,
+// loop start, loop end and after its stores drained, into a.workspace (4 x 8 B per workgroup, if non-null)
+#ifndef PICO_FWD_WGSTAMP
+#define PICO_FWD_WGSTAMP 0
+#endif
+
+// PICO_FWD_SNAKE: causal block order. The grid is dispatched in rounds of one workgroup per CU; when every
+// workgroup is resident at once (C2: 1024 = 4 per CU) each CU keeps the blocks one round hands it, so a
+// plain heaviest-first order gives the CUs that take the heaviest block of every round 40 tiles and the
+// others 32. Odd rounds run lightest-first instead (a snake over the sorted list): 36 tiles on every CU.
+#ifndef PICO_FWD_SNAKE
+#define PICO_FWD_SNAKE 1
+#endif
+
 #ifndef PICO_FWD_NBUF_D64
 #define PICO_FWD_NBUF_D64 2
 #endif
@@ -96,7 +113,7 @@ PICO_DEV float halves_sum(float x) {
 
 template <int D, bool CAUSAL>
 __global__ __launch_bounds__(256, FwdCfg<D>::WAVES_PER_EU)
-__attribute__((amdgpu_waves_per_eu(FwdCfg<D>::WAVES_PER_EU, FwdCfg<D>::WAVES_PER_EU))) void attn_fwd_kernel(const pico_attn_args a, float scale_log2) {
+__attribute__((amdgpu_waves_per_eu(FwdCfg<D>::WAVES_PER_EU, FwdCfg<D>::WAVES_PER_EU))) void attn_fwd_kernel(const pico_attn_args a, float scale_log2, int round_len) {
   using C = FwdCfg<D>;
   constexpr bool EARLY_V = PICO_FWD_EARLY_V < 0 ? D == 128 : PICO_FWD_EARLY_V != 0;
   constexpr int KS = C::KS;  // k-steps of the S^T product
@@ -106,11 +123,19 @@ __attribute__((amdgpu_waves_per_eu(FwdCfg<D>::WAVES_PER_EU, FwdCfg<D>::WAVES_PER
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (scalar branches)
   const int r = lane & 31, h = lane >> 5;
+#if PICO_FWD_WGSTAMP
+  unsigned long long wgs[4];
+  wgs[0] = __builtin_amdgcn_s_memrealtime();
+#endif
 
-  // LPT order: heaviest query blocks of every head first.
+  // LPT order: heaviest query blocks of every head first (snaked per dispatch round, PICO_FWD_SNAKE).
   const int nmb = (int)((a.seqlen_q + BM - 1) / BM);
   const int nbh = (int)(a.batch * a.heads_q);
-  const int lin = blockIdx.x;
+  int lin = blockIdx.x;
+  if (PICO_FWD_SNAKE && CAUSAL) {
+    const int rnd = lin / round_len, pos = lin - rnd * round_len;
+    if (rnd & 1) lin = rnd * round_len + min(round_len, (int)gridDim.x - rnd * round_len) - 1 - pos;
+  }
   const int mb = CAUSAL ? (nmb - 1 - lin / nbh) : (lin / nbh);
   const int bh = lin % nbh;
   const int b = bh / (int)a.heads_q;
@@ -230,8 +255,8 @@ __attribute__((amdgpu_waves_per_eu(FwdCfg<D>::WAVES_PER_EU, FwdCfg<D>::WAVES_PER
   };
 
   // One 64-key tile for this wave. MASK: apply key <= lim_lane (causal) and key < Sk.
-  auto tile_body = [&](const char* kb, unsigned vaddr, int n0, bool mask) __attribute__((always_inline)) {
-    f32x16 s[2];
+  // S^T of one 64-key tile (2 x 16 accumulators), masked when MASK
+  auto compute_s = [&](const char* kb, int n0, bool mask, f32x16 (&s)[2]) __attribute__((always_inline)) {
     // every K fragment of the tile requested before the first MFMA (one LDS latency per tile, not per step)
     bf16x8 kf[2][KS];
 #pragma unroll
@@ -246,11 +271,6 @@ __attribute__((amdgpu_waves_per_eu(FwdCfg<D>::WAVES_PER_EU, FwdCfg<D>::WAVES_PER
     }
     __builtin_amdgcn_sched_group_barrier(0x100, 2 * KS, 0);  // the K reads first,
     __builtin_amdgcn_sched_group_barrier(0x008, 2 * KS, 0);  // then the S MFMAs
-    bf16x8 vf0[2][DT], vf1[2][DT];
-    if constexpr (EARLY_V) {  // in flight during the softmax VALU below
-      v_reads(vf0, vaddr, std::integral_constant<int, 0>{});
-      v_reads(vf1, vaddr, std::integral_constant<int, 1>{});
-    }
     // lane holds row my_q, keys n0 + 32 kt + acc_row(i, h) = n0 + 4h + c(kt, i)
     if (mask) {  // wave-uniform
       const int rel = lim_lane - n0 - 4 * h;  // key allowed iff c <= rel
@@ -261,6 +281,17 @@ __attribute__((amdgpu_waves_per_eu(FwdCfg<D>::WAVES_PER_EU, FwdCfg<D>::WAVES_PER
           const int c = 32 * kt + (i & 3) + 8 * (i >> 2);
           s[kt][i] = c <= rel ? s[kt][i] : -INFINITY;
         }
+    }
+  };
+
+  // One 64-key tile for this wave. MASK: apply key <= lim_lane (causal) and key < Sk.
+  auto tile_body = [&](const char* kb, unsigned vaddr, int n0, bool mask) __attribute__((always_inline)) {
+    f32x16 s[2];
+    compute_s(kb, n0, mask, s);
+    bf16x8 vf0[2][DT], vf1[2][DT];
+    if constexpr (EARLY_V) {  // in flight during the softmax VALU below
+      v_reads(vf0, vaddr, std::integral_constant<int, 0>{});
+      v_reads(vf1, vaddr, std::integral_constant<int, 1>{});
     }
     float mx = s[0][0];
 #pragma unroll
@@ -309,6 +340,10 @@ __attribute__((amdgpu_waves_per_eu(FwdCfg<D>::WAVES_PER_EU, FwdCfg<D>::WAVES_PER
   for (int t = 0; t < P; ++t)
     if (t < ntiles) issue(t);
 
+#if PICO_FWD_WGSTAMP
+  wgs[1] = __builtin_amdgcn_s_memrealtime();
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+#endif
   for (int t = 0; t < ntiles; ++t) {
     // tile t's pieces landed (this wave's), then every wave's (barrier); later tiles stay in flight
     if (P == 2 && t + 1 < ntiles) {
@@ -329,6 +364,10 @@ __attribute__((amdgpu_waves_per_eu(FwdCfg<D>::WAVES_PER_EU, FwdCfg<D>::WAVES_PER
     }
   }
 
+#if PICO_FWD_WGSTAMP
+  wgs[2] = __builtin_amdgcn_s_memrealtime();
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+#endif
   // ---- epilogue: O = O^T / l, LSE = (m + log2 l) * ln2 ----
   // Every lane stays (the 16-byte O stores exchange half-chunks between lanes l and l + 32; only rows
   // < Sq store). O^T (for the out-projection's wgrad) is staged transposed in the now idle LDS ring,
@@ -371,6 +410,13 @@ __attribute__((amdgpu_waves_per_eu(FwdCfg<D>::WAVES_PER_EU, FwdCfg<D>::WAVES_PER
     const float lse = l_tot > 0.f ? (m_i + __log2f(l_tot)) * LN2 : -INFINITY;
     a.lse[((int64_t)b * a.heads_q + hq) * Sq + my_q] = lse;
   }
+#if PICO_FWD_WGSTAMP
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  wgs[3] = __builtin_amdgcn_s_memrealtime();
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  if (a.workspace && wave == 0 && lane < 4) ((unsigned long long*)a.workspace)[blockIdx.x * 4 + lane] = wgs[lane & 3];
+#endif
 }
 
 template <int D>
@@ -380,10 +426,11 @@ int launch_fwd(const pico_attn_args* a, hipStream_t s) {
   PICO_REQUIRE(nblk < (1ll << 31), "pico_attn_fwd: grid too large");
   const float sl2 = a->softmax_scale * LOG2E;
   PICO_REQUIRE(sl2 > 0.f, "pico_attn_fwd: softmax_scale must be positive");
+  const int rl = pico_num_cus();
   if (a->causal) {
-    PICO_LAUNCH(PICO_K_ATTN_FWD, "attn_fwd", s, attn_fwd_kernel<D, true><<<(int)nblk, 256, 0, s>>>(*a, sl2));
+    PICO_LAUNCH(PICO_K_ATTN_FWD, "attn_fwd", s, attn_fwd_kernel<D, true><<<(int)nblk, 256, 0, s>>>(*a, sl2, rl));
   } else {
-    PICO_LAUNCH(PICO_K_ATTN_FWD, "attn_fwd", s, attn_fwd_kernel<D, false><<<(int)nblk, 256, 0, s>>>(*a, sl2));
+    PICO_LAUNCH(PICO_K_ATTN_FWD, "attn_fwd", s, attn_fwd_kernel<D, false><<<(int)nblk, 256, 0, s>>>(*a, sl2, rl));
   }
   return 0;
 }

@@ -79,3 +79,16 @@ __host__ __device__ __forceinline__ void static_for(F&& f) {
 }
 
 static inline int pico_cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
+
+// compute units of the current device (cached per device; 256 on MI355X)
+static inline int pico_num_cus() {
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cached[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cached[dev] = n;
+  }
+  return cached[dev];
+}
