@@ -132,9 +132,10 @@ __attribute__((amdgpu_waves_per_eu(FwdCfg<D>::WAVES_PER_EU, FwdCfg<D>::WAVES_PER
   const int nmb = (int)((a.seqlen_q + BM - 1) / BM);
   const int nbh = (int)(a.batch * a.heads_q);
   int lin = blockIdx.x;
-  if (PICO_FWD_SNAKE && CAUSAL) {
+  if (PICO_FWD_SNAKE && CAUSAL) {  // reversed in groups of 8 (blockIdx % 8 = the XCD stays lin % 8: the
+    // blocks of one head keep sharing one XCD's L2); full rounds only
     const int rnd = lin / round_len, pos = lin - rnd * round_len;
-    if (rnd & 1) lin = rnd * round_len + min(round_len, (int)gridDim.x - rnd * round_len) - 1 - pos;
+    if ((rnd & 1) && (rnd + 1) * round_len <= (int)gridDim.x) lin = rnd * round_len + (round_len - 8 - (pos & ~7)) + (pos & 7);
   }
   const int mb = CAUSAL ? (nmb - 1 - lin / nbh) : (lin / nbh);
   const int bh = lin % nbh;
@@ -426,7 +427,7 @@ int launch_fwd(const pico_attn_args* a, hipStream_t s) {
   PICO_REQUIRE(nblk < (1ll << 31), "pico_attn_fwd: grid too large");
   const float sl2 = a->softmax_scale * LOG2E;
   PICO_REQUIRE(sl2 > 0.f, "pico_attn_fwd: softmax_scale must be positive");
-  const int rl = pico_num_cus();
+  const int rl = pico_num_cus() / 8 * 8 > 0 ? pico_num_cus() / 8 * 8 : 8;  // snake rounds: whole XCD groups
   if (a->causal) {
     PICO_LAUNCH(PICO_K_ATTN_FWD, "attn_fwd", s, attn_fwd_kernel<D, true><<<(int)nblk, 256, 0, s>>>(*a, sl2, rl));
   } else {

@@ -44,8 +44,8 @@ def main():
     lin = np.arange(nwg)
     if causal and os.getenv("PICO_FWD_SNAKE", "1") != "0":  # mirror the kernel's snake (rounds of 256 CUs)
         rnd, pos = lin // 256, lin % 256
-        odd = (rnd & 1) == 1
-        lin = np.where(odd, rnd * 256 + np.minimum(256, nwg - rnd * 256) - 1 - pos, lin)
+        odd = ((rnd & 1) == 1) & ((rnd + 1) * 256 <= nwg)
+        lin = np.where(odd, rnd * 256 + (256 - 8 - (pos & ~7)) + (pos & 7), lin)
     mb = (nmb - 1 - lin // nbh) if causal else lin // nbh
     tiles = 2 * (mb + 1) if causal else np.full(nwg, S // 64)
     per_tile = {int(m): round(float((loop[mb == m] / tiles[mb == m]).mean()), 3) for m in range(nmb)}
