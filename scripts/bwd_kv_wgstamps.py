@@ -45,7 +45,14 @@ def main():
     life = st[:, 3] - st[:, 0]
     ts = np.linspace(0, span, 200)
     resident = [int(((st[:, 0] <= t) & (st[:, 3] > t)).sum()) for t in ts]
+    kb = np.arange(nwg) // (B * H)  # hsplit 1 at C2: block id = kb * B * Hkv + bh
+    nkb = S // 128
+    by_kb = {int(k): {"start": round(float(st[kb == k, 0].mean()), 2), "end": round(float(st[kb == k, 3].mean()), 2),
+                      "pro": round(float(pro[kb == k].mean()), 2),
+                      "loop_per_tile": round(float(loop[kb == k].mean()) / ((S - 128 * k) // 32), 3)}
+             for k in range(nkb)}
     print(json.dumps({"workgroups": int(nwg), "span_us": round(span, 2), "prologue_us": round(pro.mean(), 2),
+                      "by_key_block": by_kb,
                       "loop_us": round(loop.mean(), 2), "epilogue_us": round(epi.mean(), 2),
                       "loop_share_of_wg_time": round(loop.sum() / life.sum(), 3),
                       "mean_resident": round(float(np.mean(resident)), 1), "resident_profile": resident[::10],
