@@ -59,6 +59,10 @@
 // workgroup is resident at once (C2: 1024 = 4 per CU) each CU keeps the blocks one round hands it, so a
 // plain heaviest-first order gives the CUs that take the heaviest block of every round 40 tiles and the
 // others 32. Odd rounds run lightest-first instead (a snake over the sorted list): 36 tiles on every CU.
+// PICO_FWD_PRIO: s_setprio level around each MFMA burst (0 = off). Measured C2 32.4 -> 32.7 us at 1 or 3.
+#ifndef PICO_FWD_PRIO
+#define PICO_FWD_PRIO 0
+#endif
 #ifndef PICO_FWD_SNAKE
 #define PICO_FWD_SNAKE 1
 #endif
@@ -242,6 +246,22 @@ __attribute__((amdgpu_waves_per_eu(FwdCfg<D>::WAVES_PER_EU, FwdCfg<D>::WAVES_PER
       });
     });
   };
+  // PICO_FWD_PRIO: raise the wave's issue priority around its MFMA bursts (the matrix pipe is fed first,
+  // the co-resident waves' softmax VALU fills the gaps)
+  auto prio_up = [&]() __attribute__((always_inline)) {
+    if (PICO_FWD_PRIO) {
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(PICO_FWD_PRIO);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  auto prio_down = [&]() __attribute__((always_inline)) {
+    if (PICO_FWD_PRIO) {
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
   // P^T (keys 32 kt .. 32 kt + 31 of the tile) times V: 2 * DT MFMAs.
   auto pv_mfma = [&](const f32x16& p, const bf16x8 (&vf)[2][DT]) __attribute__((always_inline)) {
     float pv[16];
@@ -249,13 +269,14 @@ __attribute__((amdgpu_waves_per_eu(FwdCfg<D>::WAVES_PER_EU, FwdCfg<D>::WAVES_PER
     for (int j = 0; j < 16; ++j) pv[j] = p[j];
     const bf16x8 pf0 = pack_bf16x8(pv), pf1 = pack_bf16x8(pv + 8);  // one v_cvt_pk_bf16_f32 per pair
     lds_wait_all();
+    prio_up();
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) o[dt] = mfma32(vf[0][dt], pf0, o[dt]);
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) o[dt] = mfma32(vf[1][dt], pf1, o[dt]);
+    prio_down();
   };
 
-  // One 64-key tile for this wave. MASK: apply key <= lim_lane (causal) and key < Sk.
   // S^T of one 64-key tile (2 x 16 accumulators), masked when MASK
   auto compute_s = [&](const char* kb, int n0, bool mask, f32x16 (&s)[2]) __attribute__((always_inline)) {
     // every K fragment of the tile requested before the first MFMA (one LDS latency per tile, not per step)
@@ -264,6 +285,7 @@ __attribute__((amdgpu_waves_per_eu(FwdCfg<D>::WAVES_PER_EU, FwdCfg<D>::WAVES_PER
     for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) kf[kt][ks] = lds_read_b128(kb, ks * C::KIMG + kt * 32 * 32);
+    prio_up();
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
       s[kt] = (f32x16)0.f;
@@ -272,6 +294,7 @@ __attribute__((amdgpu_waves_per_eu(FwdCfg<D>::WAVES_PER_EU, FwdCfg<D>::WAVES_PER
     }
     __builtin_amdgcn_sched_group_barrier(0x100, 2 * KS, 0);  // the K reads first,
     __builtin_amdgcn_sched_group_barrier(0x008, 2 * KS, 0);  // then the S MFMAs
+    prio_down();
     // lane holds row my_q, keys n0 + 32 kt + acc_row(i, h) = n0 + 4h + c(kt, i)
     if (mask) {  // wave-uniform
       const int rel = lim_lane - n0 - 4 * h;  // key allowed iff c <= rel
