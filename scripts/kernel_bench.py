@@ -30,6 +30,7 @@ def main(iters=50):
     h = torch.empty(T, I, dtype=bf, device=dev)
     dh = torch.randn(T, I, dtype=bf, device=dev)
     dgu = torch.empty_like(gu)
+    ht = torch.empty(I, T, dtype=bf, device=dev)
     ids = torch.randint(0, V, (4, 1024), device=dev)
     dy_emb = torch.randn(4, 1024, H, dtype=bf, device=dev)
     gemb = torch.zeros(V, H, dtype=bf, device=dev)
@@ -61,6 +62,9 @@ def main(iters=50):
         ("swiglu", lambda: (ops._swiglu_fwd(gu, gu[:, I:], h, T, I, 2 * I, I),
                             ops._swiglu_bwd(dh, gu, gu[:, I:], dgu, dgu[:, I:], T, I, 2 * I, I)),
          [L.K_SWIGLU_FWD, L.K_SWIGLU_BWD]),
+        ("swiglu_t", lambda: L.check(L.load().pico_swiglu_fwd_t(L.ptr(gu), L.ptr(gu[:, I:]), L.ptr(h), L.ptr(ht), T, I,
+                                                                2 * I, I, T, L.stream_of(gu)), "pico_swiglu_fwd_t"),
+         [L.K_SWIGLU_FWD]),
         ("embedding", lambda: ops._embedding_bwd_into(gemb, ids, dy_emb, 1.0), [L.K_SORT_IDS, L.K_EMBEDDING_BWD]),
         ("ce_fwd_grad", run_ce, [L.K_CE_FWD]),
         ("transpose_x", lambda: ops.transpose_2d(x.detach(), out=xt), [L.K_TRANSPOSE]),
@@ -73,6 +77,7 @@ def main(iters=50):
     for name, fn, kids in cases:
         if L.K_TRANSPOSE in kids:
             work[L.K_TRANSPOSE] = tbytes[name]
+        work[L.K_SWIGLU_FWD] = (4 if name == "swiglu_t" else 3) * T * I * 2
         for _ in range(3):
             fn()
         torch.cuda.synchronize()
@@ -84,7 +89,7 @@ def main(iters=50):
         for k in kids:
             ms, n = L.prof_collect(k)
             us = 1e3 * ms / max(n, 1)
-            out = {"kernel": L.KERNEL_NAMES[k] + ("" if k not in (L.K_TRANSPOSE,) and name != "rmsnorm_t" else ":" + name), "avg_us": round(us, 2), "launches": n}
+            out = {"kernel": L.KERNEL_NAMES[k] + ("" if k not in (L.K_TRANSPOSE,) and name not in ("rmsnorm_t", "swiglu_t") else ":" + name), "avg_us": round(us, 2), "launches": n}
             if k in work:
                 out["GB_s"] = round(work[k] / (us * 1e-6) / 1e9, 1)
                 out["frac_of_8TBs"] = round(out["GB_s"] / 8000, 3)
