@@ -80,7 +80,12 @@ constexpr int STAMP_T = 48, STAMP_P = 5;
 #ifndef PICO_BWDKV_WGSTAMP
 #define PICO_BWDKV_WGSTAMP 0
 #endif
-constexpr int64_t STAMP_BYTES = PICO_BWDKV_STAMP ? 8 * STAMP_T * STAMP_P * 8 : (PICO_BWDKV_WGSTAMP ? 65536 * 4 * 8 : 0);
+// PICO_BWDQ_WGSTAMP: the same four stamps for every dQ workgroup (same workspace tail)
+#ifndef PICO_BWDQ_WGSTAMP
+#define PICO_BWDQ_WGSTAMP 0
+#endif
+constexpr int64_t STAMP_BYTES = PICO_BWDKV_STAMP ? 8 * STAMP_T * STAMP_P * 8
+                                                 : ((PICO_BWDKV_WGSTAMP || PICO_BWDQ_WGSTAMP) ? 65536 * 4 * 8 : 0);
 
 #ifndef PICO_BWDQ_NBUF
 #define PICO_BWDQ_NBUF 3
@@ -153,8 +158,13 @@ PICO_DEV void tr_offsets(int lane, unsigned (&tro)[D / 32][2]) {
 template <int D, bool CAUSAL>
 __global__ __launch_bounds__(256, PICO_BWDQ_MINB) void attn_bwd_q_kernel(const pico_attn_args a, float scale, float scale_log2,
                                                              float* __restrict__ lse2_g, float* __restrict__ delta_g,
-                                                             int sq_pad) {
+                                                             int sq_pad, unsigned long long* __restrict__ stamp_out,
+                                                             int nfront) {
   using C = QCfg<D>;
+#if PICO_BWDQ_WGSTAMP
+  unsigned long long wgs[4];
+  wgs[0] = __builtin_amdgcn_s_memrealtime();
+#endif
   constexpr int KS = C::KS, DT = C::DT, RB = C::RB;
   __shared__ __attribute__((aligned(16))) char smem[C::NBUF * C::SLOT];
 
@@ -163,11 +173,16 @@ __global__ __launch_bounds__(256, PICO_BWDQ_MINB) void attn_bwd_q_kernel(const p
   const int r = lane & 31, h = lane >> 5;
   const int Sq = (int)a.seqlen_q, Sk = (int)a.seqlen_k;
 
-  // heaviest query blocks of every head first (causal); a head's blocks sit nbh block ids apart
+  // causal dispatch order (a head's blocks sit nbh block ids apart): the `nfront` lightest query blocks
+  // first, then the rest heaviest-first. nfront = the blocks a heaviest-first order leaves for after the
+  // first round of resident workgroups: run there, in a near-empty chip, each paid its whole prologue
+  // latency alone (C2: blocks 0-1 started at 27-29 us and ended at 36 of 40); run first (oldest, so
+  // favoured by the SIMD arbitration) they finish early and hand their slots to the heavy blocks.
   const int nmb = (Sq + QB - 1) / QB;
   const int nbh = (int)(a.batch * a.heads_q);
   const int lin = blockIdx.x;
-  const int mb = CAUSAL ? (nmb - 1 - lin / nbh) : (lin / nbh);
+  const int gi = lin / nbh;
+  const int mb = !CAUSAL ? gi : (gi < nfront ? gi : nmb - 1 - (gi - nfront));
   const int bh = lin % nbh;
   const int b = bh / (int)a.heads_q, hq = bh % (int)a.heads_q;
   const int hk = hq / (int)(a.heads_q / a.heads_kv);
@@ -374,6 +389,10 @@ __global__ __launch_bounds__(256, PICO_BWDQ_MINB) void attn_bwd_q_kernel(const p
 
 #endif
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // prologue tiles and loads landed
+#if PICO_BWDQ_WGSTAMP
+  wgs[1] = __builtin_amdgcn_s_memrealtime();
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+#endif
   // unrolled by the ring depth: every LDS read of a tile has a compile-time slot (immediate offsets)
   for (int t0 = 0; t0 < ntiles; t0 += C::NBUF) {
 #pragma unroll
@@ -397,6 +416,10 @@ __global__ __launch_bounds__(256, PICO_BWDQ_MINB) void attn_bwd_q_kernel(const p
     }
   }
 
+#if PICO_BWDQ_WGSTAMP
+  wgs[2] = __builtin_amdgcn_s_memrealtime();
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+#endif
   // ---- epilogue: lane = query my_q, register i of tile dt = d 32 dt + acc_row(i, h) ----
   // (every lane stays: the bf16 store's lane exchange needs the whole wave; only row_ok lanes store)
   if (a.flags & PICO_ATTN_ROPE_BWD) {  // rotate back by -theta: pairs (d, d + D/2) = tiles (dt, dt + DT/2)
@@ -432,6 +455,13 @@ __global__ __launch_bounds__(256, PICO_BWDQ_MINB) void attn_bwd_q_kernel(const p
   }
   bf16_t* dst = (bf16_t*)a.dq + b * a.dq_strides[0] + hq * a.dq_strides[2] + (int64_t)qc * a.dq_strides[1];
   store_row_bf16_x16<DT>(dst, h, row_ok, [&](int dt, int i) { return dq[dt][i] * scale; });
+#if PICO_BWDQ_WGSTAMP
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  wgs[3] = __builtin_amdgcn_s_memrealtime();
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  if (wave == 0 && lane < 4 && blockIdx.x < 65536) stamp_out[blockIdx.x * 4 + lane] = wgs[lane & 3];
+#endif
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -976,6 +1006,19 @@ int kv_hsplit(const pico_attn_args* a) {
 int64_t pico_attn_bwd_split_workspace(const pico_attn_args* a);
 namespace {
 
+// dQ kernel: query blocks dispatched lightest-first (see attn_bwd_q_kernel); PICO_BWDQ_FRONT < 0: automatic
+#ifndef PICO_BWDQ_FRONT
+#define PICO_BWDQ_FRONT -1
+#endif
+int q_front(const pico_attn_args* a) {
+  if (!a->causal) return 0;
+  const int nmb = (int)((a->seqlen_q + QB - 1) / QB);
+  if (PICO_BWDQ_FRONT >= 0) return PICO_BWDQ_FRONT < nmb ? PICO_BWDQ_FRONT : nmb;
+  const int64_t nbh = a->batch * a->heads_q;
+  const int64_t first = (int64_t)pico_num_cus() * PICO_BWDQ_MINB / (nbh > 0 ? nbh : 1);  // groups resident at once
+  return first < nmb ? (int)(nmb - first) : 0;
+}
+
 template <bool CAUSAL>
 int launch_split(const pico_attn_args* a, hipStream_t s) {
   constexpr int D = 64;
@@ -988,7 +1031,10 @@ int launch_split(const pico_attn_args* a, hipStream_t s) {
   const int64_t gq = (int64_t)nmb * a->batch * a->heads_q;
   PICO_REQUIRE(gq < (1ll << 31), "pico_attn_bwd: grid too large");
   PICO_LAUNCH(PICO_K_ATTN_BWD_Q, "attn_bwd_q", s,
-              attn_bwd_q_kernel<D, CAUSAL><<<(int)gq, 256, 0, s>>>(*a, a->softmax_scale, sl2, lse2, delta, sq_pad));
+              attn_bwd_q_kernel<D, CAUSAL><<<(int)gq, 256, 0, s>>>(
+                  *a, a->softmax_scale, sl2, lse2, delta, sq_pad,
+                  (unsigned long long*)((char*)a->workspace + pico_attn_bwd_split_workspace(a) - STAMP_BYTES),
+                  q_front(a)));
   const int nkb = (int)((a->seqlen_k + KVB - 1) / KVB);
   const int hsplit = kv_hsplit(a);
   const int64_t nblk = (int64_t)nkb * a->batch * a->heads_kv * hsplit;
