@@ -93,6 +93,6 @@ extern "C" int pico_adamw_bf16(const int64_t* tensors, const int64_t* sizes, con
   h.bc2_sqrt = sqrt(bc2);
   h.step_size = (float)((double)lr / bc1);
   hipStream_t s = (hipStream_t)stream;
-  PICO_LAUNCH(PICO_K_ADAMW, "adamw", s, adamw_bf16_kernel<<<(int)n_chunks, 256, 0, s>>>(tensors, sizes, chunks, h));
+  PICO_TRY(pico_launch(PICO_K_ADAMW, "adamw", adamw_bf16_kernel, dim3((int)n_chunks), dim3(256), 0, s, tensors, sizes, chunks, h));
   return 0;
 }

@@ -798,8 +798,7 @@ int launch_bwd(const pico_attn_args* a, hipStream_t s) {
   const int rope_dk = (a->flags & PICO_ATTN_ROPE_BWD) && hsplit_for(a) == 1;
   const int64_t kv_rows = rope_dk ? a->batch * a->seqlen_k * a->heads_kv : 0;
   const int pre_blocks = pico_cdiv(a->batch * a->heads_q * (int64_t)sq_pad * (D / 8), 256);
-  PICO_LAUNCH(PICO_K_ATTN_BWD_PRE, "attn_bwd_pre", s,
-              attn_bwd_pre_kernel<D><<<pre_blocks, 256, 0, s>>>(*a, delta, lse2, sq_pad));
+  PICO_TRY(pico_launch(PICO_K_ATTN_BWD_PRE, "attn_bwd_pre", attn_bwd_pre_kernel<D>, dim3(pre_blocks), dim3(256), 0, s, *a, delta, lse2, sq_pad));
   const int hsplit = hsplit_for(a);
   // fp32 dK/dV partials (hsplit > 1) after the trash slot, the diagnostic stamps and dq32
   float* dkv_part = hsplit > 1 ? trash + 64 + STAMP_BYTES / 4 + (dq32 ? slab : 0) : nullptr;
@@ -818,35 +817,28 @@ int launch_bwd(const pico_attn_args* a, hipStream_t s) {
     const int64_t nblk = (int64_t)n * a->batch * a->heads_kv * hsplit;
     if (nblk > 0) {
       if (a->causal) {
-        PICO_LAUNCH(PICO_K_ATTN_BWD, "attn_bwd", s,
-                    attn_bwd_kernel<D, true><<<(int)nblk, BwdCfg<D>::NTH, 0, s>>>(
-                        *a, a->softmax_scale, sl2, delta, lse2, sq_pad, dq_part, slab, trash, hsplit, dkv_part, kb0));
+        PICO_TRY(pico_launch(PICO_K_ATTN_BWD, "attn_bwd", attn_bwd_kernel<D, true>, dim3((int)nblk), dim3(BwdCfg<D>::NTH), 0, s, *a, a->softmax_scale, sl2, delta, lse2, sq_pad, dq_part, slab, trash, hsplit, dkv_part, kb0));
       } else {
-        PICO_LAUNCH(PICO_K_ATTN_BWD, "attn_bwd", s,
-                    attn_bwd_kernel<D, false><<<(int)nblk, BwdCfg<D>::NTH, 0, s>>>(
-                        *a, a->softmax_scale, sl2, delta, lse2, sq_pad, dq_part, slab, trash, hsplit, dkv_part, kb0));
+        PICO_TRY(pico_launch(PICO_K_ATTN_BWD, "attn_bwd", attn_bwd_kernel<D, false>, dim3((int)nblk), dim3(BwdCfg<D>::NTH), 0, s, *a, a->softmax_scale, sl2, delta, lse2, sq_pad, dq_part, slab, trash, hsplit, dkv_part, kb0));
       }
     }
     const int rdk = (g == ngroups - 1) ? rope_dk : 0;
     const int row_blocks = pico_cdiv((rows + (rdk ? kv_rows : 0)) * (D / 16), 256);
     if (a->causal) {
-      PICO_LAUNCH(PICO_K_ATTN_BWD_DQ, "attn_bwd_dq", s,
-                  attn_bwd_dq_kernel<D, true><<<row_blocks, 256, 0, s>>>(ag, dq_part, slab, n, acc, rdk, kb0));
+      PICO_TRY(pico_launch(PICO_K_ATTN_BWD_DQ, "attn_bwd_dq", attn_bwd_dq_kernel<D, true>, dim3(row_blocks), dim3(256), 0, s, ag, dq_part, slab, n, acc, rdk, kb0));
     } else {
-      PICO_LAUNCH(PICO_K_ATTN_BWD_DQ, "attn_bwd_dq", s,
-                  attn_bwd_dq_kernel<D, false><<<row_blocks, 256, 0, s>>>(ag, dq_part, slab, n, acc, rdk, kb0));
+      PICO_TRY(pico_launch(PICO_K_ATTN_BWD_DQ, "attn_bwd_dq", attn_bwd_dq_kernel<D, false>, dim3(row_blocks), dim3(256), 0, s, ag, dq_part, slab, n, acc, rdk, kb0));
     }
   }
   if (hsplit > 1 && nkb > 0) {
     const int kv_blocks = pico_cdiv(a->batch * a->seqlen_k * a->heads_kv * (D / 16), 256);
-    PICO_LAUNCH(PICO_K_ATTN_BWD_DKV, "attn_bwd_dkv", s, attn_bwd_dkv_kernel<D><<<kv_blocks, 256, 0, s>>>(*a, dkv_part, hsplit));
+    PICO_TRY(pico_launch(PICO_K_ATTN_BWD_DKV, "attn_bwd_dkv", attn_bwd_dkv_kernel<D>, dim3(kv_blocks), dim3(256), 0, s, *a, dkv_part, hsplit));
   }
   if (dq32) {  // dq32 (RoPE^-1 already applied per group: the rotation is linear) -> the caller's bf16 dQ
     pico_attn_args ac = *a;
     ac.flags = 0;
     const int row_blocks = pico_cdiv(rows * (D / 16), 256);
-    PICO_LAUNCH(PICO_K_ATTN_BWD_DQ, "attn_bwd_dq", s,
-                attn_bwd_dq_kernel<D, false><<<row_blocks, 256, 0, s>>>(ac, dq32, slab, 1, 0, 0, 0));
+    PICO_TRY(pico_launch(PICO_K_ATTN_BWD_DQ, "attn_bwd_dq", attn_bwd_dq_kernel<D, false>, dim3(row_blocks), dim3(256), 0, s, ac, dq32, slab, 1, 0, 0, 0));
   }
   return 0;
 }

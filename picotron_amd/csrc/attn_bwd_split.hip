@@ -1047,9 +1047,7 @@ int launch_split(const pico_attn_args* a, hipStream_t s) {
   const int nmb = (int)((a->seqlen_q + QB - 1) / QB);
   const int64_t gq = (int64_t)nmb * a->batch * a->heads_q;
   PICO_REQUIRE(gq < (1ll << 31), "pico_attn_bwd: grid too large");
-  PICO_LAUNCH(PICO_K_ATTN_BWD_Q, "attn_bwd_q", s,
-              attn_bwd_q_kernel<D, CAUSAL><<<(int)gq, 256, 0, s>>>(
-                  *a, a->softmax_scale, sl2, lse2, delta, sq_pad,
+  PICO_TRY(pico_launch(PICO_K_ATTN_BWD_Q, "attn_bwd_q", attn_bwd_q_kernel<D, CAUSAL>, dim3((int)gq), dim3(256), 0, s, *a, a->softmax_scale, sl2, lse2, delta, sq_pad,
                   (unsigned long long*)((char*)a->workspace + pico_attn_bwd_split_workspace(a) - STAMP_BYTES),
                   q_front(a)));
   const int nkb = (int)((a->seqlen_k + KVB - 1) / KVB);
@@ -1058,18 +1056,13 @@ int launch_split(const pico_attn_args* a, hipStream_t s) {
   if (nblk == 0) return 0;
   unsigned long long* stamps = (unsigned long long*)((char*)a->workspace + pico_attn_bwd_split_workspace(a) - STAMP_BYTES);
   if (CAUSAL && kv_minb(a) == 3) {
-    PICO_LAUNCH(PICO_K_ATTN_BWD_KV, "attn_bwd_kv", s,
-                attn_bwd_kv_kernel<D, CAUSAL, 3><<<(int)nblk, KNW * 64, 0, s>>>(
-                    *a, a->softmax_scale, sl2, lse2, delta, sq_pad, hsplit, dkv_part, stamps, kv_front(a, hsplit)));
+    PICO_TRY(pico_launch(PICO_K_ATTN_BWD_KV, "attn_bwd_kv", attn_bwd_kv_kernel<D, CAUSAL, 3>, dim3((int)nblk), dim3(KNW * 64), 0, s, *a, a->softmax_scale, sl2, lse2, delta, sq_pad, hsplit, dkv_part, stamps, kv_front(a, hsplit)));
   } else {
-    PICO_LAUNCH(PICO_K_ATTN_BWD_KV, "attn_bwd_kv", s,
-                attn_bwd_kv_kernel<D, CAUSAL, 2><<<(int)nblk, KNW * 64, 0, s>>>(
-                    *a, a->softmax_scale, sl2, lse2, delta, sq_pad, hsplit, dkv_part, stamps, kv_front(a, hsplit)));
+    PICO_TRY(pico_launch(PICO_K_ATTN_BWD_KV, "attn_bwd_kv", attn_bwd_kv_kernel<D, CAUSAL, 2>, dim3((int)nblk), dim3(KNW * 64), 0, s, *a, a->softmax_scale, sl2, lse2, delta, sq_pad, hsplit, dkv_part, stamps, kv_front(a, hsplit)));
   }
   if (hsplit > 1) {
     const int kv_blocks = pico_cdiv(a->batch * a->seqlen_k * a->heads_kv * (D / 16), 256);
-    PICO_LAUNCH(PICO_K_ATTN_BWD_DKV, "attn_bwd_dkv", s,
-                attn_bwd_dkv_kernel<D><<<kv_blocks, 256, 0, s>>>(*a, dkv_part, hsplit));
+    PICO_TRY(pico_launch(PICO_K_ATTN_BWD_DKV, "attn_bwd_dkv", attn_bwd_dkv_kernel<D>, dim3(kv_blocks), dim3(256), 0, s, *a, dkv_part, hsplit));
   }
   return 0;
 }

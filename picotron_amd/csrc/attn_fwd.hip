@@ -452,9 +452,9 @@ int launch_fwd(const pico_attn_args* a, hipStream_t s) {
   PICO_REQUIRE(sl2 > 0.f, "pico_attn_fwd: softmax_scale must be positive");
   const int rl = pico_num_cus() / 8 * 8 > 0 ? pico_num_cus() / 8 * 8 : 8;  // snake rounds: whole XCD groups
   if (a->causal) {
-    PICO_LAUNCH(PICO_K_ATTN_FWD, "attn_fwd", s, attn_fwd_kernel<D, true><<<(int)nblk, 256, 0, s>>>(*a, sl2, rl));
+    PICO_TRY(pico_launch(PICO_K_ATTN_FWD, "attn_fwd", attn_fwd_kernel<D, true>, dim3((int)nblk), dim3(256), 0, s, *a, sl2, rl));
   } else {
-    PICO_LAUNCH(PICO_K_ATTN_FWD, "attn_fwd", s, attn_fwd_kernel<D, false><<<(int)nblk, 256, 0, s>>>(*a, sl2, rl));
+    PICO_TRY(pico_launch(PICO_K_ATTN_FWD, "attn_fwd", attn_fwd_kernel<D, false>, dim3((int)nblk), dim3(256), 0, s, *a, sl2, rl));
   }
   return 0;
 }

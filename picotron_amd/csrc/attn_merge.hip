@@ -67,9 +67,7 @@ extern "C" int pico_attn_merge(float* out, float* lse, const void* block_out, co
   const int64_t threads = batch * seqlen * heads * (head_dim / 8);
   if (threads == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
-  PICO_LAUNCH(PICO_K_ATTN_MERGE, "attn_merge", s,
-              attn_merge_kernel<<<pico_cdiv(threads, 256), 256, 0, s>>>(
-                  out, lse, (const bf16_t*)block_out, block_lse, (int)batch, (int)seqlen, (int)heads, (int)head_dim,
+  PICO_TRY(pico_launch(PICO_K_ATTN_MERGE, "attn_merge", attn_merge_kernel, dim3(pico_cdiv(threads, 256)), dim3(256), 0, s, out, lse, (const bf16_t*)block_out, block_lse, (int)batch, (int)seqlen, (int)heads, (int)head_dim,
                   bo_strides[0], bo_strides[1], bo_strides[2], first));
   return 0;
 }

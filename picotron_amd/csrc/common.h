@@ -3,6 +3,7 @@
 // caller's hipStream_t and never allocates (workspaces come from the caller).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 
 #include <type_traits>
@@ -33,27 +34,40 @@ PICO_DEV unsigned pack2bf(float lo, float hi) {
 }
 
 // ---------------------------------------------------------------------------------------
-// Host-side status / profiling plumbing (defined in runtime.cpp)
+// Host-side status / profiling plumbing (defined in runtime.hip)
 // ---------------------------------------------------------------------------------------
 int pico_set_error(const char* fmt, ...);
 int pico_check_launch(const char* op);
-void pico_prof_pre(int kid, hipStream_t s);
-void pico_prof_post(int kid, hipStream_t s);
+// true when kernel id `kid` is being timed: *start / *stop are the next free event pair of its pool
+bool pico_prof_events(int kid, hipEvent_t* start, hipEvent_t* stop);
 
 #define PICO_REQUIRE(cond, ...)               \
   do {                                        \
     if (!(cond)) return pico_set_error(__VA_ARGS__); \
   } while (0)
 
-// Launch wrapper: optional event timing of one kernel id, then error check.
-#define PICO_LAUNCH(kid, opname, stream, ...)          \
-  do {                                                 \
-    pico_prof_pre((kid), (stream));                    \
-    __VA_ARGS__;                                       \
-    pico_prof_post((kid), (stream));                   \
-    int _rc = pico_check_launch(opname);               \
-    if (_rc) return _rc;                               \
+#define PICO_TRY(expr)         \
+  do {                         \
+    const int _rc = (expr);    \
+    if (_rc) return _rc;       \
   } while (0)
+
+// Every kernel launch of the library: the arguments are converted to the kernel's parameter types; while
+// kernel id `kid` is timed (pico_prof_enable) the launch carries its own start / stop events
+// (hipExtLaunchKernel: the dispatch packet's timestamps, i.e. the kernel's execution time as rocprofv3
+// reports it, without the queue gap a pair of stream-recorded events would add); then the error check.
+template <typename... KP, typename... Args>
+int pico_launch(int kid, const char* op, void (*kernel)(KP...), dim3 grid, dim3 block, unsigned shmem, hipStream_t s,
+                Args&&... args) {
+  static_assert(sizeof...(KP) == sizeof...(Args), "pico_launch: argument count");
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (pico_prof_events(kid, &e0, &e1)) {
+    hipExtLaunchKernelGGL(kernel, grid, block, shmem, s, e0, e1, 0u, static_cast<KP>(args)...);
+  } else {
+    kernel<<<grid, block, shmem, s>>>(static_cast<KP>(args)...);
+  }
+  return pico_check_launch(op);
+}
 
 // Sum over the 64 lanes of a wave, result in every lane, without LDS (ds_bpermute) round trips:
 // DPP within rows of 16 (quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror), then

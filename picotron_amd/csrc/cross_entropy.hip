@@ -213,8 +213,7 @@ extern "C" int pico_cross_entropy_fwd(const void* logits, int64_t ld, const int6
   if (rows == 0) return 0;
   PICO_REQUIRE(logits && target && lse && loss, "pico_cross_entropy_fwd: null pointer");
   hipStream_t s = (hipStream_t)stream;
-  CE_SWITCH(nch, PICO_LAUNCH(PICO_K_CE_FWD, "cross_entropy_fwd", s,
-                             ce_fwd_kernel<N><<<(int)rows, 256, 0, s>>>((const bf16_t*)logits, ld, target, lse, loss,
+  CE_SWITCH(nch, PICO_TRY(pico_launch(PICO_K_CE_FWD, "cross_entropy_fwd", ce_fwd_kernel<N>, dim3((int)rows), dim3(256), 0, s, (const bf16_t*)logits, ld, target, lse, loss,
                                                                         (int)vocab, ignore_index)))
   return 0;
 }
@@ -230,8 +229,7 @@ extern "C" int pico_cross_entropy_fwd_grad(void* logits, int64_t ld, const int64
   if (rows == 0) return 0;
   PICO_REQUIRE(logits && target && lse && loss && grad_scale, "pico_cross_entropy_fwd_grad: null pointer");
   hipStream_t s = (hipStream_t)stream;
-  CE_SWITCH(nch, PICO_LAUNCH(PICO_K_CE_FWD, "cross_entropy_fwd_grad", s,
-                             ce_fwd_grad_kernel<N, PICO_CE_THREADS><<<(int)rows, PICO_CE_THREADS, 0, s>>>((bf16_t*)logits, ld, target, lse, loss,
+  CE_SWITCH(nch, PICO_TRY(pico_launch(PICO_K_CE_FWD, "cross_entropy_fwd_grad", ce_fwd_grad_kernel<N, PICO_CE_THREADS>, dim3((int)rows), dim3(PICO_CE_THREADS), 0, s, (bf16_t*)logits, ld, target, lse, loss,
                                                                              grad_scale, (int)vocab, ignore_index)))
   return 0;
 }
@@ -246,8 +244,7 @@ extern "C" int pico_cross_entropy_bwd(const void* logits, int64_t ld, const int6
   if (rows == 0) return 0;
   PICO_REQUIRE(logits && target && lse && grad_scale && dlogits, "pico_cross_entropy_bwd: null pointer");
   hipStream_t s = (hipStream_t)stream;
-  CE_SWITCH(nch, PICO_LAUNCH(PICO_K_CE_BWD, "cross_entropy_bwd", s,
-                             ce_bwd_kernel<N><<<(int)rows, 256, 0, s>>>((const bf16_t*)logits, ld, target, lse,
+  CE_SWITCH(nch, PICO_TRY(pico_launch(PICO_K_CE_BWD, "cross_entropy_bwd", ce_bwd_kernel<N>, dim3((int)rows), dim3(256), 0, s, (const bf16_t*)logits, ld, target, lse,
                                                                         grad_scale, (bf16_t*)dlogits, ldd, (int)vocab,
                                                                         ignore_index)))
   return 0;

@@ -100,11 +100,9 @@ int pico_grad_accum(float* main_grad, const void* grad, int64_t n, float divide_
   const float inv = 1.f / divide_by;  // fp32 reciprocal, as ATen's scalar-divisor path computes it
   const bool vec = n % 8 == 0 && (uintptr_t)main_grad % 32 == 0 && (uintptr_t)grad % 16 == 0;
   if (vec) {
-    PICO_LAUNCH(PICO_K_GRAD_ACCUM, "grad_accum", s,
-                grad_accum_vec<<<grid_for(n / 8), 256, 0, s>>>(main_grad, (const bf16_t*)grad, n / 8, inv, do_div));
+    PICO_TRY(pico_launch(PICO_K_GRAD_ACCUM, "grad_accum", grad_accum_vec, dim3(grid_for(n / 8)), dim3(256), 0, s, main_grad, (const bf16_t*)grad, n / 8, inv, do_div));
   } else {
-    PICO_LAUNCH(PICO_K_GRAD_ACCUM, "grad_accum", s,
-                grad_accum_scalar<<<grid_for(n), 256, 0, s>>>(main_grad, (const bf16_t*)grad, n, inv, do_div));
+    PICO_TRY(pico_launch(PICO_K_GRAD_ACCUM, "grad_accum", grad_accum_scalar, dim3(grid_for(n)), dim3(256), 0, s, main_grad, (const bf16_t*)grad, n, inv, do_div));
   }
   return 0;
 }
@@ -115,7 +113,7 @@ int pico_scale_f32(float* buf, int64_t n, float divide_by, void* stream) {
   PICO_REQUIRE((uintptr_t)buf % 16 == 0, "pico_scale_f32: buffer must be 16-byte aligned");
   if (n <= 0 || divide_by == 1.f) return 0;
   hipStream_t s = (hipStream_t)stream;
-  PICO_LAUNCH(PICO_K_SCALE, "scale_f32", s, scale_kernel<<<grid_for(n / 4), 256, 0, s>>>(buf, n, 1.f / divide_by));
+  PICO_TRY(pico_launch(PICO_K_SCALE, "scale_f32", scale_kernel, dim3(grid_for(n / 4)), dim3(256), 0, s, buf, n, 1.f / divide_by));
   return 0;
 }
 
@@ -125,9 +123,9 @@ int pico_cast_f32_bf16(const float* src, void* dst, int64_t n, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const bool vec = n % 8 == 0 && (uintptr_t)src % 32 == 0 && (uintptr_t)dst % 16 == 0;
   if (vec) {
-    PICO_LAUNCH(PICO_K_CAST, "cast_f32_bf16", s, cast_vec<<<grid_for(n / 8), 256, 0, s>>>(src, (bf16_t*)dst, n / 8));
+    PICO_TRY(pico_launch(PICO_K_CAST, "cast_f32_bf16", cast_vec, dim3(grid_for(n / 8)), dim3(256), 0, s, src, (bf16_t*)dst, n / 8));
   } else {
-    PICO_LAUNCH(PICO_K_CAST, "cast_f32_bf16", s, cast_scalar<<<grid_for(n), 256, 0, s>>>(src, (bf16_t*)dst, n));
+    PICO_TRY(pico_launch(PICO_K_CAST, "cast_f32_bf16", cast_scalar, dim3(grid_for(n)), dim3(256), 0, s, src, (bf16_t*)dst, n));
   }
   return 0;
 }

@@ -124,8 +124,7 @@ extern "C" int pico_sort_ids(const int64_t* ids, int64_t n, int64_t vocab, int64
   int p2 = 2;
   while (p2 < n) p2 <<= 1;
   hipStream_t s = (hipStream_t)stream;
-  PICO_LAUNCH(PICO_K_SORT_IDS, "sort_ids", s,
-              sort_ids_kernel<<<1, 1024, 0, s>>>(ids, (int)n, p2, sorted_ids, sorted_pos));
+  PICO_TRY(pico_launch(PICO_K_SORT_IDS, "sort_ids", sort_ids_kernel, dim3(1), dim3(1024), 0, s, ids, (int)n, p2, sorted_ids, sorted_pos));
   return 0;
 }
 
@@ -139,12 +138,10 @@ extern "C" int pico_embedding_bwd(const int64_t* sorted_ids, const int64_t* sort
   PICO_REQUIRE(((uintptr_t)dy | (uintptr_t)grad) % 16 == 0, "pico_embedding_bwd: dy/grad must be 16-byte aligned");
   hipStream_t s = (hipStream_t)stream;
   if (grad_is_f32) {
-    PICO_LAUNCH(PICO_K_EMBEDDING_BWD, "embedding_bwd", s,
-                embedding_bwd_kernel<true><<<(int)n_tokens, 256, 0, s>>>(sorted_ids, sorted_pos, (const bf16_t*)dy,
+    PICO_TRY(pico_launch(PICO_K_EMBEDDING_BWD, "embedding_bwd", embedding_bwd_kernel<true>, dim3((int)n_tokens), dim3(256), 0, s, sorted_ids, sorted_pos, (const bf16_t*)dy,
                                                                          grad, n_tokens, dim, scale));
   } else {
-    PICO_LAUNCH(PICO_K_EMBEDDING_BWD, "embedding_bwd", s,
-                embedding_bwd_kernel<false><<<(int)n_tokens, 256, 0, s>>>(sorted_ids, sorted_pos, (const bf16_t*)dy,
+    PICO_TRY(pico_launch(PICO_K_EMBEDDING_BWD, "embedding_bwd", embedding_bwd_kernel<false>, dim3((int)n_tokens), dim3(256), 0, s, sorted_ids, sorted_pos, (const bf16_t*)dy,
                                                                           grad, n_tokens, dim, scale));
   }
   return 0;

@@ -272,10 +272,8 @@ int launch_rmsnorm_bwd(const void* dy, const void* dres, const void* x, const vo
                        float* part, int64_t rows, int c, int nb, hipStream_t s) {
   constexpr int NW = bwd_waves(M);
   auto go = [&](auto full, auto res) {
-    PICO_LAUNCH(PICO_K_RMSNORM_BWD, "rmsnorm_bwd", s,
-                (rmsnorm_bwd_kernel<M, NW, decltype(full)::value, decltype(res)::value><<<nb, NW * 64, 0, s>>>(
-                    (const bf16_t*)dy, (const bf16_t*)dres, (const bf16_t*)x, (const bf16_t*)w, rstd, (bf16_t*)dx,
-                    part, rows, c)));
+    PICO_TRY(pico_launch(PICO_K_RMSNORM_BWD, "rmsnorm_bwd", rmsnorm_bwd_kernel<M, NW, decltype(full)::value, decltype(res)::value>, dim3(nb), dim3(NW * 64), 0, s, (const bf16_t*)dy, (const bf16_t*)dres, (const bf16_t*)x, (const bf16_t*)w, rstd, (bf16_t*)dx,
+                    part, rows, c));
     return 0;
   };
   const bool full = c == M * 512;
@@ -372,8 +370,7 @@ int pico_rmsnorm_fwd_t(const void* x, const void* residual, const void* weight, 
     auto k = rmsnorm_fwd_t_kernel<M, R>;
     hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return pico_set_error("pico_rmsnorm_fwd_t: cannot set LDS size (%d)", (int)e);
-    PICO_LAUNCH(PICO_K_RMSNORM_FWD, "rmsnorm_fwd_t", s,
-                k<<<nb, FWDT_WAVES * 64, lds, s>>>(xp, rp, wp, (bf16_t*)y, (bf16_t*)residual_out, rstd, (bf16_t*)y_t, ld_t, eps));
+    PICO_TRY(pico_launch(PICO_K_RMSNORM_FWD, "rmsnorm_fwd_t", k, dim3(nb), dim3(FWDT_WAVES * 64), lds, s, xp, rp, wp, (bf16_t*)y, (bf16_t*)residual_out, rstd, (bf16_t*)y_t, ld_t, eps));
     return 0;
   };
   using I2 = std::integral_constant<int, 2>;
@@ -400,7 +397,7 @@ int pico_rmsnorm_fwd(const void* x, const void* residual, const void* weight, vo
   const int c = (int)cols;
 #define FWD_CASE(M) \
   case M:           \
-    PICO_LAUNCH(PICO_K_RMSNORM_FWD, "rmsnorm_fwd", s, rmsnorm_fwd_kernel<M><<<grid, block, 0, s>>>(xp, rp, wp, yp, rop, rstd, rows, c, eps)); \
+    PICO_TRY(pico_launch(PICO_K_RMSNORM_FWD, "rmsnorm_fwd", rmsnorm_fwd_kernel<M>, dim3(grid), dim3(block), 0, s, xp, rp, wp, yp, rop, rstd, rows, c, eps)); \
     break;
   switch (mc) {
     FWD_CASE(1) FWD_CASE(2) FWD_CASE(4) FWD_CASE(8) FWD_CASE(16)
@@ -443,12 +440,11 @@ int pico_rmsnorm_bwd_acc(const void* dy, const void* dresidual, const void* x, c
 
   const int g = pico_cdiv(cols, DW_COLS);
   if (dw_mode == 0) {
-    PICO_LAUNCH(PICO_K_RMSNORM_DW, "rmsnorm_dw", s, rmsnorm_dw_kernel<0><<<g, 256, 0, s>>>(part, dweight, nb, c, 1.f));
+    PICO_TRY(pico_launch(PICO_K_RMSNORM_DW, "rmsnorm_dw", rmsnorm_dw_kernel<0>, dim3(g), dim3(256), 0, s, part, dweight, nb, c, 1.f));
   } else if (dw_mode == 1) {
-    PICO_LAUNCH(PICO_K_RMSNORM_DW, "rmsnorm_dw", s, rmsnorm_dw_kernel<1><<<g, 256, 0, s>>>(part, dweight, nb, c, 1.f));
+    PICO_TRY(pico_launch(PICO_K_RMSNORM_DW, "rmsnorm_dw", rmsnorm_dw_kernel<1>, dim3(g), dim3(256), 0, s, part, dweight, nb, c, 1.f));
   } else {
-    PICO_LAUNCH(PICO_K_RMSNORM_DW, "rmsnorm_dw", s,
-                rmsnorm_dw_kernel<2><<<g, 256, 0, s>>>(part, dweight, nb, c, dw_scale));
+    PICO_TRY(pico_launch(PICO_K_RMSNORM_DW, "rmsnorm_dw", rmsnorm_dw_kernel<2>, dim3(g), dim3(256), 0, s, part, dweight, nb, c, dw_scale));
   }
   return 0;
 }

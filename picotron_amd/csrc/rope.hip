@@ -65,8 +65,7 @@ extern "C" int pico_rope(const void* x, void* out, const void* cos, const void* 
   hipStream_t s = (hipStream_t)stream;
   int64_t nb = (total + 255) / 256;
   if (nb > 8192) nb = 8192;
-  PICO_LAUNCH(PICO_K_ROPE, "rope", s,
-              rope_kernel<<<(int)nb, 256, 0, s>>>((const bf16_t*)x, (bf16_t*)out, (const bf16_t*)cos,
+  PICO_TRY(pico_launch(PICO_K_ROPE, "rope", rope_kernel, dim3((int)nb), dim3(256), 0, s, (const bf16_t*)x, (bf16_t*)out, (const bf16_t*)cos,
                                                   (const bf16_t*)sin, total, (int)seqlen, (int)heads,
                                                   (int)(head_dim / 2), xst[0], xst[1], xst[2], ost[0], ost[1], ost[2],
                                                   cs_stride, conjugate ? -1.f : 1.f));

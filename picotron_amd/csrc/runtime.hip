@@ -2,7 +2,8 @@
 //
 // The timer lets bench.py measure each kernel's average launch duration live, on the stream the
 // kernel is launched on (torch.cuda.Event only sees torch's current stream): while enabled, every
-// launch of an enabled kernel id is bracketed by a pair of pre-created hipEvents.
+// launch of an enabled kernel id carries a pair of pre-created hipEvents as its start / stop events
+// (pico_launch in common.h).
 #include <stdarg.h>
 #include <stdio.h>
 #include <atomic>
@@ -46,21 +47,15 @@ void destroy_pool(Pool& p) {
 }
 }  // namespace
 
-void pico_prof_pre(int kid, hipStream_t s) {
-  if (!(g_mask.load(std::memory_order_relaxed) & (1u << kid))) return;
+bool pico_prof_events(int kid, hipEvent_t* start, hipEvent_t* stop) {
+  if (!(g_mask.load(std::memory_order_relaxed) & (1u << kid))) return false;
   std::lock_guard<std::mutex> lk(g_mu);
   Pool& p = g_pool[kid];
-  if (p.used >= p.capacity) return;
-  (void)hipEventRecord(p.ev[2 * p.used], s);
-}
-
-void pico_prof_post(int kid, hipStream_t s) {
-  if (!(g_mask.load(std::memory_order_relaxed) & (1u << kid))) return;
-  std::lock_guard<std::mutex> lk(g_mu);
-  Pool& p = g_pool[kid];
-  if (p.used >= p.capacity) return;
-  (void)hipEventRecord(p.ev[2 * p.used + 1], s);
+  if (p.used >= p.capacity) return false;
+  *start = p.ev[2 * p.used];
+  *stop = p.ev[2 * p.used + 1];
   p.used++;
+  return true;
 }
 
 extern "C" {

@@ -166,8 +166,7 @@ int pico_swiglu_fwd_t(const void* gate, const void* up, void* out, void* out_t, 
   if (rows == 0 || cols == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   dim3 grid((unsigned)(cols / 64), (unsigned)(rows / 64));
-  PICO_LAUNCH(PICO_K_SWIGLU_FWD, "swiglu_fwd_t", s,
-              swiglu_fwd_t_kernel<<<grid, 256, 0, s>>>((const bf16_t*)gate, (const bf16_t*)up, (bf16_t*)out,
+  PICO_TRY(pico_launch(PICO_K_SWIGLU_FWD, "swiglu_fwd_t", swiglu_fwd_t_kernel, dim3(grid), dim3(256), 0, s, (const bf16_t*)gate, (const bf16_t*)up, (bf16_t*)out,
                                                        (bf16_t*)out_t, in_stride, out_stride, t_stride));
   return 0;
 }
@@ -184,12 +183,10 @@ int pico_swiglu_fwd(const void* gate, const void* up, void* out, int64_t rows, i
   auto u = (const bf16_t*)up;
   auto h = (bf16_t*)out;
   if (vec_ok(cols, in_stride, out_stride, gate, up, out)) {
-    PICO_LAUNCH(PICO_K_SWIGLU_FWD, "swiglu_fwd", s,
-                swiglu_fwd_kernel<<<grid_for(rows * cols / 8), 256, 0, s>>>(g, u, h, rows, (int)cols, in_stride,
+    PICO_TRY(pico_launch(PICO_K_SWIGLU_FWD, "swiglu_fwd", swiglu_fwd_kernel, dim3(grid_for(rows * cols / 8)), dim3(256), 0, s, g, u, h, rows, (int)cols, in_stride,
                                                                              out_stride));
   } else {
-    PICO_LAUNCH(PICO_K_SWIGLU_FWD, "swiglu_fwd", s,
-                swiglu_fwd_scalar<<<grid_for(rows * cols), 256, 0, s>>>(g, u, h, rows, (int)cols, in_stride,
+    PICO_TRY(pico_launch(PICO_K_SWIGLU_FWD, "swiglu_fwd", swiglu_fwd_scalar, dim3(grid_for(rows * cols)), dim3(256), 0, s, g, u, h, rows, (int)cols, in_stride,
                                                                         out_stride));
   }
   return 0;
@@ -206,14 +203,10 @@ int pico_swiglu_bwd(const void* dout, const void* gate, const void* up, void* dg
   const bool vec = vec_ok(cols, in_stride, out_stride, dout, gate, up) &&
                    ((uintptr_t)dgate | (uintptr_t)dup) % 16 == 0;
   if (vec) {
-    PICO_LAUNCH(PICO_K_SWIGLU_BWD, "swiglu_bwd", s,
-                swiglu_bwd_kernel<<<grid_for(rows * cols / 8), 256, 0, s>>>(
-                    (const bf16_t*)dout, (const bf16_t*)gate, (const bf16_t*)up, (bf16_t*)dgate, (bf16_t*)dup, rows,
+    PICO_TRY(pico_launch(PICO_K_SWIGLU_BWD, "swiglu_bwd", swiglu_bwd_kernel, dim3(grid_for(rows * cols / 8)), dim3(256), 0, s, (const bf16_t*)dout, (const bf16_t*)gate, (const bf16_t*)up, (bf16_t*)dgate, (bf16_t*)dup, rows,
                     (int)cols, in_stride, out_stride));
   } else {
-    PICO_LAUNCH(PICO_K_SWIGLU_BWD, "swiglu_bwd", s,
-                swiglu_bwd_scalar<<<grid_for(rows * cols), 256, 0, s>>>(
-                    (const bf16_t*)dout, (const bf16_t*)gate, (const bf16_t*)up, (bf16_t*)dgate, (bf16_t*)dup, rows,
+    PICO_TRY(pico_launch(PICO_K_SWIGLU_BWD, "swiglu_bwd", swiglu_bwd_scalar, dim3(grid_for(rows * cols)), dim3(256), 0, s, (const bf16_t*)dout, (const bf16_t*)gate, (const bf16_t*)up, (bf16_t*)dgate, (bf16_t*)dup, rows,
                     (int)cols, in_stride, out_stride));
   }
   return 0;

@@ -69,8 +69,7 @@ extern "C" int pico_transpose_bf16(const void* src, int64_t ld_src, void* dst, i
   PICO_REQUIRE((rows + TT - 1) / TT <= 65535, "pico_transpose_bf16: too many rows");
   hipStream_t s = (hipStream_t)stream;
   dim3 grid((unsigned)pico_cdiv(cols, TT), (unsigned)pico_cdiv(rows, TT));
-  PICO_LAUNCH(PICO_K_TRANSPOSE, "transpose_bf16", s,
-              transpose_bf16_kernel<<<grid, 256, 0, s>>>((const bf16_t*)src, ld_src, (bf16_t*)dst, ld_dst, rows,
+  PICO_TRY(pico_launch(PICO_K_TRANSPOSE, "transpose_bf16", transpose_bf16_kernel, dim3(grid), dim3(256), 0, s, (const bf16_t*)src, ld_src, (bf16_t*)dst, ld_dst, rows,
                                                          cols));
   return 0;
 }
