@@ -54,6 +54,15 @@ def main():
         torch.cuda.synchronize()
         fl = 4.0 * B * Hq * S * S * D * (0.5 if causal else 1.0)
         res = {"config": name, "B": B, "S": S, "Hq": Hq, "Hkv": Hkv, "D": D, "causal": causal}
+        # wall time of the whole backward call on the caller's stream (kernel timers off): with the
+        # concurrent split form (PICO_ATTN_CONC=1) the sum of kernel times overstates it
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(args.iters):
+            ops.attention_block_bwd(do, q, k, v, o, lse, sc, causal)
+        e1.record()
+        torch.cuda.synchronize()
+        res["bwd_wall_us"] = round(1e3 * e0.elapsed_time(e1) / args.iters, 2)
         tot_bwd = 0.0
         for i in ids:
             ms, n = L.prof_collect(i)
@@ -66,6 +75,7 @@ def main():
         main = res["attn_bwd_us"] or res["attn_bwd_kv_us"]
         res["bwd_kernel_tflops"] = round(2.5 * fl / (main * 1e-6) / 1e12, 1) if main else None
         res["bwd_total_tflops"] = round(2.5 * fl / (tot_bwd * 1e-6) / 1e12, 1)
+        res["bwd_wall_tflops"] = round(2.5 * fl / (res["bwd_wall_us"] * 1e-6) / 1e12, 1)
         res["fwd_bwd_tflops"] = round(3.5 * fl / ((res["attn_fwd_us"] + tot_bwd) * 1e-6) / 1e12, 1)
         print(json.dumps(res), flush=True)
 
