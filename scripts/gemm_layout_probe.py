@@ -43,7 +43,7 @@ def main():
         print(json.dumps(r), flush=True)
 
 
-if __name__ == "__main__" and "--wgrad" not in __import__("sys").argv and "--fwd" not in __import__("sys").argv:
+if __name__ == "__main__" and not {"--wgrad", "--fwd", "--dyt"} & set(__import__("sys").argv):
     main()
 
 
@@ -88,3 +88,28 @@ def fwd_main():
 
 if __name__ == "__main__" and "--fwd" in __import__("sys").argv:
     fwd_main()
+
+
+def dyt_main():
+    """Everything a layer's backward would issue if the producer of dy wrote ONLY dy^T ([N, T]):
+    dgrad dx = dy W from dy^T (two forms) against the current form F.linear(dy, W^T), and the wgrad
+    accumulation dW += dy^T x in the NT form (dy^T, x^T given) against the current TT form (dy, x^T)."""
+    torch.manual_seed(0)
+    for name, (N, K) in SHAPES.items():
+        x = torch.randn(T, K, device="cuda", dtype=torch.bfloat16)
+        w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.02
+        wt = w.t().contiguous()
+        dy = torch.randn(T, N, device="cuda", dtype=torch.bfloat16)
+        xt, dyt = x.t().contiguous(), dy.t().contiguous()
+        g = torch.zeros(N, K, device="cuda", dtype=torch.bfloat16)
+        r = {"shape": name, "N": N, "K": K}
+        r["dgrad_cur_linear_dy_wt"] = bench(lambda: F.linear(dy, wt))
+        r["dgrad_dyt_mm_w"] = bench(lambda: dyt.t() @ w)
+        r["dgrad_dyt_linear_wt"] = bench(lambda: F.linear(dyt.t(), wt))
+        r["wgrad_cur_TT"] = bench(lambda: torch.addmm(g, dy.t(), xt.t(), out=g))
+        r["wgrad_NT_dyt_xt"] = bench(lambda: torch.addmm(g, dyt, xt.t(), out=g))
+        print(json.dumps(r), flush=True)
+
+
+if __name__ == "__main__" and "--dyt" in __import__("sys").argv:
+    dyt_main()
