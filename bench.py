@@ -291,6 +291,13 @@ def main():
             roofline["note"] = ("algorithmic backward FLOPs (5 products, 2.5 x forward) over the summed mean launch "
                                 "times of " + " + ".join(parts) + "; the kernels execute 7 products (S and dP "
                                 "recomputed in the dQ kernel)")
+        if "attn_fwd" in kernels and roofline["kernel"].startswith("attn_bwd"):
+            # north_star's attention target is fwd + bwd together: 3.5 x forward FLOPs over the forward's
+            # and the backward kernels' mean launch times
+            fwd_us = kernels["attn_fwd"]["avg_us"]
+            tf = 3.5 * kernel_work(L.K_ATTN_FWD, cfg, MBS, SEQ)[0] / ((fwd_us + avg_us) * 1e-6) / 1e12
+            roofline["attention_fwd_bwd"] = {"us": round(fwd_us + avg_us, 2), "achieved": round(tf, 2),
+                                             "frac": round(tf / BF16_PEAK_TFLOPS, 4)}
         for v in kernels.values():
             v["total_ms"] = round(v["total_ms"], 3)
             v["avg_us"] = round(v["avg_us"], 2)
