@@ -749,13 +749,29 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const pico_attn_args a
 
 // tile-list split of a key block (see attn_bwd_kernel): the smallest factor (<= 8) giving at least two
 // workgroups per CU (512 = one launch wave of 256 CUs x 2), at most the block's query tile count
+// Split key blocks until ONE launch (a group of at most PICO_BWD_KB_CAP key blocks) fills the chip once
+// (one workgroup per CU: the kernel's LDS), twice under GQA, whose key blocks carry G query heads' tiles and
+// need the finer split to balance (PICO_BWD_HSPLIT_GRID = 0: this rule). Filling it twice without GQA (the
+// round-1 rule: 512 workgroups over all key blocks) doubled the fp32 dK/dV partials for no faster main kernel
+// — Llama-2-7B/tp2 per rank (B 2, 16 heads, D 128, S 1024): causal 117.9 -> 105.9 us, non-causal 148.8 ->
+// 117.3 us for the whole backward; GQA-4 at the same shape: 164.5 (8 parts) vs 167.8 (4 parts); counting every
+// key block instead of one launch's would leave a grouped launch (S 4096) half the chip.
+#ifndef PICO_BWD_KB_CAP
+#define PICO_BWD_KB_CAP 8
+#endif
+#ifndef PICO_BWD_HSPLIT_GRID
+#define PICO_BWD_HSPLIT_GRID 0
+#endif
 int hsplit_for(const pico_attn_args* a) {
   if (a->heads_kv <= 0 || a->heads_q % a->heads_kv != 0) return 1;  // rejected by the argument checks
-  const int64_t nblk = ((a->seqlen_k + BK - 1) / BK) * a->batch * a->heads_kv;
+  const int64_t nkb = (a->seqlen_k + BK - 1) / BK;
+  const int64_t nblk = (nkb < PICO_BWD_KB_CAP ? nkb : PICO_BWD_KB_CAP) * a->batch * a->heads_kv;  // per launch
   const int64_t tiles = (a->heads_q / a->heads_kv) * ((a->seqlen_q + BQ - 1) / BQ);  // of key block 0
   if (nblk <= 0) return 1;
+  const int64_t grid = PICO_BWD_HSPLIT_GRID > 0 ? PICO_BWD_HSPLIT_GRID
+                                                : (int64_t)pico_num_cus() * (a->heads_q > a->heads_kv ? 2 : 1);
   int d = 1;
-  while (d < 8 && nblk * d < 512 && 2 * d <= tiles) d *= 2;
+  while (d < 8 && nblk * d < grid && 2 * d <= tiles) d *= 2;
   return d;
 }
 
@@ -767,12 +783,9 @@ int64_t lsd_floats(const pico_attn_args* a) {
   return ((n + 63) / 64) * 64;
 }
 
-// Key blocks per launch of the fused kernel: its dQ partial slabs (one fp32 [B, Sq, Hq, D] per key block)
-// are bounded by this many; longer sequences run the key blocks in groups, each group's slab sum added
-// into an fp32 dQ (the slab workspace grew as S^2 / 256)
-#ifndef PICO_BWD_KB_CAP
-#define PICO_BWD_KB_CAP 8
-#endif
+// Key blocks per launch of the fused kernel (PICO_BWD_KB_CAP, above): its dQ partial slabs (one fp32
+// [B, Sq, Hq, D] per key block) are bounded by this many; longer sequences run the key blocks in groups, each
+// group's slab sum added into an fp32 dQ (the slab workspace grew as S^2 / 256)
 int kb_groups(const pico_attn_args* a) {
   const int64_t nkb = (a->seqlen_k + BK - 1) / BK;
   return (int)((nkb + PICO_BWD_KB_CAP - 1) / PICO_BWD_KB_CAP);

@@ -21,6 +21,9 @@ CONFIGS = {
     "d128": (2, 1024, 16, 16, 128, True),   # Llama-2-7B per TP rank (tp2), micro-batch 2
     "gqa4": (4, 1024, 32, 8, 64, True),
     "s4096": (1, 4096, 32, 32, 64, True),   # CP block size of config 5
+    "d128_full": (2, 1024, 16, 16, 128, False),
+    "d128_s4096": (1, 4096, 16, 16, 128, True),
+    "d128_gqa4": (2, 1024, 32, 8, 128, True),
 }
 
 
