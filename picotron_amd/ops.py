@@ -437,6 +437,38 @@ def dgrad(dy2, W, params):
     return torch.matmul(dy2, W)
 
 
+def _conc_tags():
+    """PICO_WGRAD_CONC: comma list of {o (square plain projections), lin (other plain), qkv, gu} or 'all' / 'none':
+    the wgrad GEMM of those projections runs on a side stream beside their dgrad GEMM and is joined right after
+    it. Default 'gu': the gate|up pair (dgrad [T, Hd] with K = 2I fills half the chip for a long K loop, the
+    wgrad [2I, Hd] fills the rest) measured 866.0 -> 862.8 ms per C2 step (2 rounds x 2 boxes); the out / down /
+    qkv pairs measured slower side by side (+0.5-0.9 % per step)."""
+    v = os.getenv("PICO_WGRAD_CONC", "gu")
+    if v == "none":
+        return set()
+    return {"o", "lin", "qkv", "gu"} if v == "all" else set(t for t in v.split(",") if t)
+
+
+_SIDE = {}
+
+
+def dgrad_wgrad(tag, dy2, W, params, x2):
+    """(dx, wgrad_accumulate(...)) for one projection; concurrently on two streams when `tag` is enabled."""
+    if tag in _conc_tags() and dy2.is_cuda:
+        dev = dy2.device
+        cur = torch.cuda.current_stream(dev)
+        side = _SIDE.get(dev)
+        if side is None:
+            side = _SIDE[dev] = torch.cuda.Stream(device=dev)
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            dws = wgrad_accumulate(params, dy2, x2)
+        dx = dgrad(dy2, W, params)
+        cur.wait_stream(side)
+        return dx, dws
+    return dgrad(dy2, W, params), wgrad_accumulate(params, dy2, x2)
+
+
 def sort_ids(flat, vocab):
     """torch.sort(flat, stable=True) of int64 token ids on pico_sort_ids (one LDS workgroup) when it fits
     (<= 8192 ids, vocab <= 2^19); the same result, bit for bit."""
@@ -730,6 +762,9 @@ class _LinearFn(torch.autograd.Function):
     def backward(ctx, dy):
         x2, w = ctx.saved_tensors
         dy2 = dy.reshape(-1, dy.shape[-1])
+        if ctx.needs_input_grad[0] and ctx.needs_input_grad[1]:
+            dx, (dw,) = dgrad_wgrad("o" if w.shape[0] == w.shape[1] else "lin", dy2, w, (w,), x2)
+            return dx.view(ctx.xshape), dw
         dx = dgrad(dy2, w, (w,)).view(ctx.xshape) if ctx.needs_input_grad[0] else None
         dw = wgrad_accumulate((w,), dy2, x2)[0] if ctx.needs_input_grad[1] else None
         return dx, dw
@@ -809,9 +844,8 @@ class _GateUpSwiGLUFn(torch.autograd.Function):
             d = d.contiguous()
         dgu = torch.empty_like(gu)
         _swiglu_bwd(d, gu, gu[:, I:], dgu, dgu[:, I:], gu.shape[0], I, 2 * I, I)
-        dx = dgrad(dgu, W, ctx.params).view(ctx.xshape)
-        dwg, dwu = wgrad_accumulate(ctx.params, dgu, x2)
-        return dx, dwg, dwu
+        dx, (dwg, dwu) = dgrad_wgrad("gu", dgu, W, ctx.params, x2)
+        return dx.view(ctx.xshape), dwg, dwu
 
 
 def gate_up_swiglu(x, w_gate, w_up):
@@ -983,9 +1017,8 @@ class _QKVRopeAttentionFn(torch.autograd.Function):
         if not fused:
             dqk = dheads[:, :, : nh + nkv]
             _rope_launch(dqk, dqk, cos, sin, True)
-        dx = dgrad(dqkv, W, ctx.params).view(B, S, Hd)
-        dwq, dwk, dwv = wgrad_accumulate(ctx.params, dqkv, x2)
-        return dx, dwq, dwk, dwv, None, None, None, None, None
+        dx, (dwq, dwk, dwv) = dgrad_wgrad("qkv", dqkv, W, ctx.params, x2)
+        return dx.view(B, S, Hd), dwq, dwk, dwv, None, None, None, None, None
 
 
 def qkv_rope_attention(x, wq, wk, wv, cos, sin, num_heads, num_kv_heads, causal):
