@@ -14,6 +14,7 @@ Extra entry points used by picotron_amd's own modules:
     attention_block_fwd / attention_block_bwd - ring-attention block fwd/bwd with fp32 LSE
                                                 (ref picotron/context_parallel/context_parallel.py:112-155)
 """
+import contextlib
 import ctypes
 import math
 import os
@@ -438,15 +439,16 @@ def dgrad(dy2, W, params):
 
 
 def _conc_tags():
-    """PICO_WGRAD_CONC: comma list of {o (square plain projections), lin (other plain), qkv, gu} or 'all' / 'none':
-    the wgrad GEMM of those projections runs on a side stream beside their dgrad GEMM and is joined right after
-    it. Default 'gu': the gate|up pair (dgrad [T, Hd] with K = 2I fills half the chip for a long K loop, the
-    wgrad [2I, Hd] fills the rest) measured 866.0 -> 862.8 ms per C2 step (2 rounds x 2 boxes); the out / down /
-    qkv pairs measured slower side by side (+0.5-0.9 % per step)."""
-    v = os.getenv("PICO_WGRAD_CONC", "gu")
+    """PICO_WGRAD_CONC: comma list of {o (square plain projections), lin (other plain), qkv, gu, lm} or 'all' /
+    'none': the wgrad GEMM of those projections runs on a side stream beside their dgrad GEMM and is joined right
+    after it. Default 'gu,lm': the gate|up pair (dgrad [T, Hd] with K = 2I fills half the chip for a long K loop,
+    the wgrad [2I, Hd] fills the rest) measured 866.0 -> 862.8 ms per C2 step (2 rounds x 2 boxes), the LM head's
+    per-chunk pair (the same shape class, K = V) 855.5 -> 855.0 (3 rounds); the out / down / qkv pairs measured
+    slower side by side (+0.5-0.9 % per step)."""
+    v = os.getenv("PICO_WGRAD_CONC", "gu,lm")
     if v == "none":
         return set()
-    return {"o", "lin", "qkv", "gu"} if v == "all" else set(t for t in v.split(",") if t)
+    return {"o", "lin", "qkv", "gu", "lm"} if v == "all" else set(t for t in v.split(",") if t)
 
 
 _SIDE = {}
@@ -667,6 +669,7 @@ class _LMHeadCEChunkedFn(torch.autograd.Function):
                 elif g.is_contiguous() and g.dtype == w.dtype and tuple(g.shape) == tuple(w.shape):
                     kind, dst = "grad", g
         lib = _lib.load()
+        conc = "lm" in _conc_tags()
         for c0 in range(0, T, chunk):
             c1 = min(T, c0 + chunk)
             n = c1 - c0
@@ -676,24 +679,35 @@ class _LMHeadCEChunkedFn(torch.autograd.Function):
                                                        _lib.ptr(loss_rows[c0:]), _lib.ptr(gscale), n, V,
                                                        int(ignore_index), _lib.stream_of(x)),
                        "pico_cross_entropy_fwd_grad")
+            # the chunk's dW GEMM on the side stream beside its dx GEMM when PICO_WGRAD_CONC has "lm" (joined
+            # before the next chunk overwrites the logits buffer)
+            side = None
+            if conc and need_w:
+                side = _SIDE.get(x.device)
+                if side is None:
+                    side = _SIDE[x.device] = torch.cuda.Stream(device=x.device)
+                side.wait_stream(torch.cuda.current_stream(x.device))
+            if need_w:
+                xc = xin[c0:c1]
+                with (torch.cuda.stream(side) if side is not None else contextlib.nullcontext()):
+                    if kind == "main":  # fp32 main_grad: 1/W folds into the first chunk's beta and every alpha
+                        torch.addmm(dst, lg.t(), xc, beta=(sc if c0 == 0 else 1.0), alpha=sc, out_dtype=torch.float32,
+                                    out=dst)
+                    elif kind in ("grad", "fresh_acc", "autograd_acc"):
+                        torch.addmm(dst, lg.t(), xc, out=dst)
+                    elif kind == "fresh":
+                        w.grad = dst = torch.mm(lg.t(), xc)
+                        kind = "fresh_acc"
+                    else:  # "autograd": a buffer handed back from the backward
+                        dst = torch.mm(lg.t(), xc)
+                        kind = "autograd_acc"
             if ctx.needs_input_grad[0]:
                 if wt is not None:
                     torch.mm(lg, wt.t(), out=dx[c0:c1])
                 else:
                     torch.mm(lg, w, out=dx[c0:c1])
-            if not need_w:
-                continue
-            xc = xin[c0:c1]
-            if kind == "main":  # fp32 main_grad: 1/W folds into the first chunk's beta and every alpha
-                torch.addmm(dst, lg.t(), xc, beta=(sc if c0 == 0 else 1.0), alpha=sc, out_dtype=torch.float32, out=dst)
-            elif kind in ("grad", "fresh_acc", "autograd_acc"):
-                torch.addmm(dst, lg.t(), xc, out=dst)
-            elif kind == "fresh":
-                w.grad = dst = torch.mm(lg.t(), xc)
-                kind = "fresh_acc"
-            else:  # "autograd": a buffer handed back from the backward
-                dst = torch.mm(lg.t(), xc)
-                kind = "autograd_acc"
+            if side is not None:
+                torch.cuda.current_stream(x.device).wait_stream(side)
         loss = loss_rows.sum() / n_valid * grad_scale
         ctx.save_for_backward(dx)
         ctx.xshape = x.shape
