@@ -106,6 +106,9 @@ def main():
                     help="process-group backend: nccl (= RCCL over xGMI, the product) or gloo (tests: several "
                          "ranks sharing one GPU, which RCCL refuses)")
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--sync-steps", action="store_true",
+                    help="read the loss on the host after every step (one device sync per step, as a per-step "
+                         "log line would) instead of once after the timed region")
     ap.add_argument("--fused-adam", type=int, default=1,
                     help="AdamW(fused=True): the reference's use_fused_adam config (ref template/base_config.json:18, "
                          "train.py:204-207)")
@@ -180,10 +183,10 @@ def main():
 
     graphs = MicroBatchGraph(model, args.grad_acc, zero_grads) if args.graphs else None
 
-    def step():
+    def step(sync=True):
         # graphs: gradient buffers must persist (zeroed in place); eager: the reference's set_to_none
         opt.zero_grad(set_to_none=graphs is None)
-        loss = train_step(model, loader, device, graphs=graphs)
+        loss = train_step(model, loader, device, graphs=graphs, sync=sync)
         opt.step()
         if hasattr(model, "reset"):
             model.reset()
@@ -210,10 +213,13 @@ def main():
     t_start = time.perf_counter()
     losses = []
     for i in range(args.steps):
-        losses.append(step())
+        # the loss stays on the device until the timed region ends: no host sync inside it (the host queues
+        # step i + 1 while the device runs step i; --sync-steps restores one .item() per step)
+        losses.append(step(sync=args.sync_steps))
     torch.cuda.synchronize()
     dist.barrier()
     elapsed = time.perf_counter() - t_start
+    losses = [float(l) for l in losses]
     t = torch.tensor([elapsed], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
