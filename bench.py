@@ -186,7 +186,7 @@ def main():
     def step(sync=True):
         # graphs: gradient buffers must persist (zeroed in place); eager: the reference's set_to_none
         opt.zero_grad(set_to_none=graphs is None)
-        loss = train_step(model, loader, device, graphs=graphs, sync=sync)
+        loss = train_step(model, loader, device, graphs=graphs, sync_loss=sync)
         opt.step()
         if hasattr(model, "reset"):
             model.reset()

@@ -112,6 +112,21 @@ int pico_rmsnorm_bwd(const void* dy, const void* dresidual, const void* x, const
 int pico_rmsnorm_bwd_acc(const void* dy, const void* dresidual, const void* x, const void* weight,
                          const float* rstd, void* dx, void* dweight, int dw_mode, float dw_scale,
                          void* workspace, int64_t rows, int64_t cols, void* stream);
+/* Chained form (one launch per norm instead of two): as pico_rmsnorm_bwd_acc, but
+ *   reduce_own = 0 leaves this call's dw partial rows (pico_rmsnorm_bwd_partial_rows of them, [nb][cols]
+ *     fp32) in `workspace` for a later call to reduce (dweight / dw_mode / dw_scale unused);
+ *   prev_part != NULL: the same launch also reduces a previous call's partial rows ([prev_nb][prev_cols],
+ *     still alive in the caller's memory) into prev_dweight with prev_mode / prev_scale.
+ * pico_rmsnorm_dw_reduce does that reduction alone (the last norm of a backward pass). Deterministic: every
+ * dw sum runs in a fixed order. */
+int pico_rmsnorm_bwd_chain(const void* dy, const void* dresidual, const void* x, const void* weight,
+                           const float* rstd, void* dx, void* dweight, int dw_mode, float dw_scale,
+                           void* workspace, int64_t rows, int64_t cols, int reduce_own,
+                           const float* prev_part, int64_t prev_nb, int64_t prev_cols, void* prev_dweight,
+                           int prev_mode, float prev_scale, void* stream);
+int64_t pico_rmsnorm_bwd_partial_rows(int64_t rows, int64_t cols);
+int pico_rmsnorm_dw_reduce(const float* part, int64_t nb, int64_t cols, void* dweight, int dw_mode,
+                           float dw_scale, void* stream);
 
 /* ---- RoPE, rotate-half (non-interleaved) layout ----
  * x, out: [batch, seqlen, heads, head_dim] bf16 with element strides (batch, seq, head) and

@@ -62,6 +62,11 @@ _SIGNATURES = {
     "pico_rmsnorm_bwd": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp]),
     "pico_rmsnorm_bwd_acc": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.c_int, ctypes.c_float,
                                             c_vp, c_i64, c_i64, c_vp]),
+    "pico_rmsnorm_bwd_chain": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.c_int, ctypes.c_float,
+                                              c_vp, c_i64, c_i64, ctypes.c_int, c_vp, c_i64, c_i64, c_vp, ctypes.c_int,
+                                              ctypes.c_float, c_vp]),
+    "pico_rmsnorm_bwd_partial_rows": (c_i64, [c_i64, c_i64]),
+    "pico_rmsnorm_dw_reduce": (ctypes.c_int, [c_vp, c_i64, c_i64, c_vp, ctypes.c_int, ctypes.c_float, c_vp]),
     "pico_rope": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64,
                                  ctypes.POINTER(c_i64), ctypes.POINTER(c_i64), c_i64, ctypes.c_int, c_vp]),
     "pico_swiglu_fwd": (ctypes.c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp]),

@@ -179,6 +179,17 @@ __global__ __launch_bounds__(FWDT_WAVES * 64) void rmsnorm_fwd_t_kernel(const bf
   }
 }
 
+// A previous backward call's dw partial rows, reduced by this launch (the chained form,
+// pico_rmsnorm_bwd_chain): workgroup b sums columns [b * cpw, (b + 1) * cpw) over the `nb` partial rows in a
+// fixed order and applies the dw mode, instead of a separate launch of rmsnorm_dw_kernel.
+struct DwPrev {
+  const float* part;  // nullptr: nothing to reduce
+  void* dw;
+  int nb, cols, cpw, mode;
+  float scale;
+};
+constexpr int PREV_COLS = 16;  // column slots per workgroup (cpw <= 16)
+
 // Backward: dx = rstd * (g - xhat * mean(g * xhat)), g = dy * w, xhat = x * rstd;
 // dw partial per workgroup (deterministic two-stage reduction, no atomics).
 // FULL: cols == MAXC * 512 (every lane chunk in range: no per-chunk predicates, which otherwise
@@ -190,10 +201,23 @@ __global__ __launch_bounds__(NW * 64) void rmsnorm_bwd_kernel(const bf16_t* __re
                                                               const bf16_t* __restrict__ dres,
                                                               const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
                                                               const float* __restrict__ rstd, bf16_t* __restrict__ dx,
-                                                              float* __restrict__ dw_part, int64_t rows, int cols) {
+                                                              float* __restrict__ dw_part, int64_t rows, int cols,
+                                                              const DwPrev prev) {
   __shared__ float red[NW * MAXC * 512];  // per-wave dw partial rows (accumulated in LDS, not registers)
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
+  // chained dw of the previous call: this thread's partial rows of one column slot, loaded first (in flight
+  // during the row loop); slot c = t % 16, row group g = t / 16, rows g, g + NG, ...
+  constexpr int NG = NW * 64 / PREV_COLS, PR = 256 / NG;  // prev.nb <= 256 (host check)
+  float pv[PR];
+  const int pcs = threadIdx.x % PREV_COLS, pg = threadIdx.x / PREV_COLS;
+  const int pcol = blockIdx.x * prev.cpw + pcs;
+  const bool pok = prev.part && pcs < prev.cpw && pcol < prev.cols;
+#pragma unroll
+  for (int k = 0; k < PR; ++k) {
+    const int pr = pg + NG * k;
+    pv[k] = (pok && pr < prev.nb) ? prev.part[(int64_t)pr * prev.cols + pcol] : 0.f;
+  }
   float* myred = red + wid * MAXC * 512 + lane * 8;  // chunk c at + 512 c
 #pragma unroll
   for (int c = 0; c < MAXC; ++c) {
@@ -260,6 +284,28 @@ __global__ __launch_bounds__(NW * 64) void rmsnorm_bwd_kernel(const bf16_t* __re
     for (int k = 0; k < NW; ++k) s += red[k * MAXC * 512 + col];
     dw_part[(int64_t)blockIdx.x * cols + col] = s;
   }
+  if (prev.part) {  // workgroup-uniform: the previous call's dw, columns of this workgroup's slice
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < PR; ++k) s += pv[k];  // rows ascending
+    __syncthreads();  // every thread past its reads of red
+    red[pg * PREV_COLS + pcs] = s;
+    __syncthreads();
+    if (threadIdx.x < prev.cpw && blockIdx.x * prev.cpw + (int)threadIdx.x < prev.cols) {
+      const int col = blockIdx.x * prev.cpw + threadIdx.x;
+      float t = 0.f;
+      for (int g = 0; g < NG; ++g) t += red[g * PREV_COLS + threadIdx.x];  // groups ascending: fixed order
+      if (prev.mode == 0) {
+        ((bf16_t*)prev.dw)[col] = f2bf(t);
+      } else if (prev.mode == 1) {
+        bf16_t* q = (bf16_t*)prev.dw + col;
+        *q = f2bf(bf2f(*q) + t);
+      } else {
+        float* q = (float*)prev.dw + col;
+        *q = (*q + t) * prev.scale;
+      }
+    }
+  }
 }
 
 #ifndef PICO_RMS_BWD_NW4
@@ -269,11 +315,11 @@ constexpr int bwd_waves(int maxc) { return maxc <= 2 ? 16 : (maxc == 4 ? PICO_RM
 
 template <int M>
 int launch_rmsnorm_bwd(const void* dy, const void* dres, const void* x, const void* w, const float* rstd, void* dx,
-                       float* part, int64_t rows, int c, int nb, hipStream_t s) {
+                       float* part, int64_t rows, int c, int nb, const DwPrev& prev, hipStream_t s) {
   constexpr int NW = bwd_waves(M);
   auto go = [&](auto full, auto res) {
     PICO_TRY(pico_launch(PICO_K_RMSNORM_BWD, "rmsnorm_bwd", rmsnorm_bwd_kernel<M, NW, decltype(full)::value, decltype(res)::value>, dim3(nb), dim3(NW * 64), 0, s, (const bf16_t*)dy, (const bf16_t*)dres, (const bf16_t*)x, (const bf16_t*)w, rstd, (bf16_t*)dx,
-                    part, rows, c));
+                    part, rows, c, prev));
     return 0;
   };
   const bool full = c == M * 512;
@@ -419,7 +465,36 @@ int pico_rmsnorm_bwd(const void* dy, const void* dresidual, const void* x, const
 int pico_rmsnorm_bwd_acc(const void* dy, const void* dresidual, const void* x, const void* weight, const float* rstd,
                          void* dx, void* dweight, int dw_mode, float dw_scale, void* workspace, int64_t rows,
                          int64_t cols, void* stream) {
-  PICO_REQUIRE(dy && x && weight && rstd && dx && dweight && workspace, "pico_rmsnorm_bwd: null pointer");
+  return pico_rmsnorm_bwd_chain(dy, dresidual, x, weight, rstd, dx, dweight, dw_mode, dw_scale, workspace, rows, cols,
+                                1, nullptr, 0, 0, nullptr, 0, 1.f, stream);
+}
+
+int pico_rmsnorm_dw_reduce(const float* part, int64_t nb, int64_t cols, void* dweight, int dw_mode, float dw_scale,
+                           void* stream) {
+  PICO_REQUIRE(part && dweight, "pico_rmsnorm_dw_reduce: null pointer");
+  PICO_REQUIRE(dw_mode >= 0 && dw_mode <= 2, "pico_rmsnorm_dw_reduce: dw_mode %d not in 0..2", dw_mode);
+  PICO_REQUIRE(nb > 0 && cols > 0 && nb < (1 << 30) && cols < (1 << 30), "pico_rmsnorm_dw_reduce: bad shape");
+  hipStream_t s = (hipStream_t)stream;
+  const int g = pico_cdiv(cols, DW_COLS), n = (int)nb, c = (int)cols;
+  if (dw_mode == 0) {
+    PICO_TRY(pico_launch(PICO_K_RMSNORM_DW, "rmsnorm_dw", rmsnorm_dw_kernel<0>, dim3(g), dim3(256), 0, s, part, dweight, n, c, 1.f));
+  } else if (dw_mode == 1) {
+    PICO_TRY(pico_launch(PICO_K_RMSNORM_DW, "rmsnorm_dw", rmsnorm_dw_kernel<1>, dim3(g), dim3(256), 0, s, part, dweight, n, c, 1.f));
+  } else {
+    PICO_TRY(pico_launch(PICO_K_RMSNORM_DW, "rmsnorm_dw", rmsnorm_dw_kernel<2>, dim3(g), dim3(256), 0, s, part, dweight, n, c, dw_scale));
+  }
+  return 0;
+}
+
+int64_t pico_rmsnorm_bwd_partial_rows(int64_t rows, int64_t cols) {
+  return maxc_for(cols) > 0 ? bwd_blocks(rows, cols) : 0;
+}
+
+int pico_rmsnorm_bwd_chain(const void* dy, const void* dresidual, const void* x, const void* weight, const float* rstd,
+                           void* dx, void* dweight, int dw_mode, float dw_scale, void* workspace, int64_t rows,
+                           int64_t cols, int reduce_own, const float* prev_part, int64_t prev_nb, int64_t prev_cols,
+                           void* prev_dweight, int prev_mode, float prev_scale, void* stream) {
+  PICO_REQUIRE(dy && x && weight && rstd && dx && workspace && (dweight || !reduce_own), "pico_rmsnorm_bwd: null pointer");
   PICO_REQUIRE(dw_mode >= 0 && dw_mode <= 2, "pico_rmsnorm_bwd_acc: dw_mode %d not in 0..2", dw_mode);
   PICO_REQUIRE(rows > 0 && cols > 0 && cols % 8 == 0, "pico_rmsnorm_bwd: bad shape rows=%lld cols=%lld",
                (long long)rows, (long long)cols);
@@ -427,25 +502,28 @@ int pico_rmsnorm_bwd_acc(const void* dy, const void* dresidual, const void* x, c
   PICO_REQUIRE(mc > 0 && mc <= 8, "pico_rmsnorm_bwd: cols=%lld > 4096 unsupported", (long long)cols);
   hipStream_t s = (hipStream_t)stream;
   const int nb = bwd_blocks(rows, cols);
+  DwPrev prev{nullptr, nullptr, 0, 0, 0, 0, 1.f};
+  if (prev_part) {
+    PICO_REQUIRE(prev_dweight && prev_mode >= 0 && prev_mode <= 2 && prev_nb > 0 && prev_nb <= 256 && prev_cols > 0,
+                 "pico_rmsnorm_bwd_chain: bad previous partials");
+    const int64_t cpw = (prev_cols + nb - 1) / nb;
+    if (cpw <= PREV_COLS) {
+      prev = DwPrev{prev_part, prev_dweight, (int)prev_nb, (int)prev_cols, (int)cpw, prev_mode, prev_scale};
+    } else {  // too many columns for this grid: reduce them in their own launch first
+      PICO_TRY(pico_rmsnorm_dw_reduce(prev_part, prev_nb, prev_cols, prev_dweight, prev_mode, prev_scale, stream));
+    }
+  }
   auto part = (float*)workspace;
   const int c = (int)cols;
   int rc = 0;
   switch (mc) {
-    case 1: rc = launch_rmsnorm_bwd<1>(dy, dresidual, x, weight, rstd, dx, part, rows, c, nb, s); break;
-    case 2: rc = launch_rmsnorm_bwd<2>(dy, dresidual, x, weight, rstd, dx, part, rows, c, nb, s); break;
-    case 4: rc = launch_rmsnorm_bwd<4>(dy, dresidual, x, weight, rstd, dx, part, rows, c, nb, s); break;
-    case 8: rc = launch_rmsnorm_bwd<8>(dy, dresidual, x, weight, rstd, dx, part, rows, c, nb, s); break;
+    case 1: rc = launch_rmsnorm_bwd<1>(dy, dresidual, x, weight, rstd, dx, part, rows, c, nb, prev, s); break;
+    case 2: rc = launch_rmsnorm_bwd<2>(dy, dresidual, x, weight, rstd, dx, part, rows, c, nb, prev, s); break;
+    case 4: rc = launch_rmsnorm_bwd<4>(dy, dresidual, x, weight, rstd, dx, part, rows, c, nb, prev, s); break;
+    case 8: rc = launch_rmsnorm_bwd<8>(dy, dresidual, x, weight, rstd, dx, part, rows, c, nb, prev, s); break;
   }
   if (rc) return rc;
-
-  const int g = pico_cdiv(cols, DW_COLS);
-  if (dw_mode == 0) {
-    PICO_TRY(pico_launch(PICO_K_RMSNORM_DW, "rmsnorm_dw", rmsnorm_dw_kernel<0>, dim3(g), dim3(256), 0, s, part, dweight, nb, c, 1.f));
-  } else if (dw_mode == 1) {
-    PICO_TRY(pico_launch(PICO_K_RMSNORM_DW, "rmsnorm_dw", rmsnorm_dw_kernel<1>, dim3(g), dim3(256), 0, s, part, dweight, nb, c, 1.f));
-  } else {
-    PICO_TRY(pico_launch(PICO_K_RMSNORM_DW, "rmsnorm_dw", rmsnorm_dw_kernel<2>, dim3(g), dim3(256), 0, s, part, dweight, nb, c, dw_scale));
-  }
+  if (reduce_own) return pico_rmsnorm_dw_reduce(part, nb, cols, dweight, dw_mode, dw_scale, stream);
   return 0;
 }
 

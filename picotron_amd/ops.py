@@ -98,13 +98,49 @@ class _RMSNormFn(torch.autograd.Function):
         mode, target, scale, ready = _norm_grad_target(ctx.weight_param, w)
         dw = target if mode == 0 else None
         ws = torch.empty(lib.pico_rmsnorm_bwd_workspace_bytes(rows, cols), dtype=torch.uint8, device=dy.device)
-        _lib.check(lib.pico_rmsnorm_bwd_acc(_lib.ptr(dy2), _lib.ptr(dres), _lib.ptr(x_eff), _lib.ptr(w),
-                                            _lib.ptr(rstd), _lib.ptr(dx), _lib.ptr(target), mode, float(scale),
-                                            _lib.ptr(ws), rows, cols, _lib.stream_of(dy)), "pico_rmsnorm_bwd")
-        if ready is not None:
+        # chained dw (one launch per norm): an in-place accumulation (mode 1 / 2) leaves its partial rows for the
+        # next norm backward of this pass to reduce; this launch reduces the previous one's
+        dev = dy.device
+        prev = _NORM_PENDING.pop(dev, None)
+        # (not with a readiness callback: the DP bucket's post-backward callback, queued before ours, would wait
+        # for a bucket whose last norm weight is still pending)
+        defer = mode != 0 and ready is None and _norm_chain_enabled()
+        _lib.check(lib.pico_rmsnorm_bwd_chain(
+            _lib.ptr(dy2), _lib.ptr(dres), _lib.ptr(x_eff), _lib.ptr(w), _lib.ptr(rstd), _lib.ptr(dx), _lib.ptr(target),
+            mode, float(scale), _lib.ptr(ws), rows, cols, 0 if defer else 1,
+            _lib.ptr(prev[0]) if prev else None, prev[1] if prev else 0, prev[2] if prev else 0,
+            _lib.ptr(prev[3]) if prev else None, prev[4] if prev else 0, float(prev[5]) if prev else 1.0,
+            _lib.stream_of(dy)), "pico_rmsnorm_bwd")
+        if prev is not None and prev[6] is not None:
+            prev[6]()  # the previous norm's weight gradient is complete now (DP bucket readiness)
+        if defer:
+            _NORM_PENDING[dev] = (ws, lib.pico_rmsnorm_bwd_partial_rows(rows, cols), cols, target, mode, scale, ready)
+            torch.autograd.Variable._execution_engine.queue_callback(lambda: _flush_norm_dw(dev))
+        elif ready is not None:
             ready()
         dx = dx.view(ctx.shape)
         return dx, (dx if ctx.has_residual else None), dw, None, None, None
+
+
+# device -> a norm backward's dw partial rows waiting for the next norm backward of the same pass to reduce them
+# (workspace, partial rows, cols, target, mode, scale, ready callback); _flush_norm_dw reduces what is left
+# when the backward pass ends
+_NORM_PENDING = {}
+
+
+def _norm_chain_enabled():
+    return os.getenv("PICO_NORM_DW_CHAIN", "1") != "0"
+
+
+def _flush_norm_dw(dev):
+    prev = _NORM_PENDING.pop(dev, None)
+    if prev is None:
+        return
+    ws, nb, cols, target, mode, scale, ready = prev
+    _lib.check(_lib.load().pico_rmsnorm_dw_reduce(_lib.ptr(ws), nb, cols, _lib.ptr(target), mode, float(scale),
+                                                  _lib.stream_of(target)), "pico_rmsnorm_dw_reduce")
+    if ready is not None:
+        ready()
 
 
 def _norm_grad_target(p, w):

@@ -56,11 +56,11 @@ def _micro_batch(model, input_ids, target_ids, grad_acc_steps):
     return loss.detach()
 
 
-def train_step(model, data_loader, device, graphs=None, sync=True):
+def train_step(model, data_loader, device, graphs=None, sync_loss=True):
     """ref train.py:29-55: grad-accumulation loop, DP sync only on the last micro-batch,
     mean CE / grad_acc_steps, returns the accumulated (python float) loss.
     `graphs` (a MicroBatchGraph) replays the micro-batches that do not sync DP gradients.
-    sync=False returns the loss as a device scalar instead: no host synchronisation in the step, so the
+    sync_loss=False returns the loss as a device scalar instead: no host synchronisation in the step, so the
     host queues the optimizer step and the next step's launches while the device still runs this one."""
     m = pgm.process_group_manager
     # the reference toggles DP sync only when cp_dp_world_size > 1; a DP wrapper at W = 1 is toggled
@@ -83,7 +83,7 @@ def train_step(model, data_loader, device, graphs=None, sync=True):
         losses.append(graphs.take_loss())
     # one host sync per step instead of one per micro-batch (ref :53 calls .item() each time), or none
     total = torch.stack(losses).float().sum() if losses else torch.zeros((), device=device)
-    return float(total.item()) if sync else total
+    return float(total.item()) if sync_loss else total
 
 
 class MicroBatchGraph:
