@@ -69,6 +69,58 @@ def test_rmsnorm_shapes(rows, cols):
         assert rel_l2(wr.grad.cpu(), dw) < 4e-3
 
 
+@pytest.mark.parametrize("cols", [2048, 4096])
+def test_rmsnorm_chained_dw(monkeypatch, cols):
+    """Three stacked norms accumulating into persistent bf16 .grad (dw_mode 1): the first two weight gradients
+    are reduced inside the NEXT norm's backward launch, the last by the end-of-backward callback
+    (pico_rmsnorm_bwd_chain / pico_rmsnorm_dw_reduce). Same values as the one-launch-per-reduction path (same
+    partial rows, fixed-order sums: within one bf16 rounding) and as the fp64 restatement, over two backward
+    passes (the second accumulates into the first's .grad)."""
+    ops = _ops()
+    torch.manual_seed(cols)
+    rows = 512
+    x0 = torch.randn(rows, cols, dtype=BF, device=DEV) * 2
+    ws = [(1 + 0.1 * torch.randn(cols, device=DEV)).to(BF) for _ in range(3)]
+    dys = [torch.randn(rows, cols, dtype=BF, device=DEV) for _ in range(2)]
+
+    def run(chain):
+        monkeypatch.setenv("PICO_NORM_DW_CHAIN", "1" if chain else "0")
+        params = [w.clone().requires_grad_(True) for w in ws]
+        for p in params:
+            p.grad = torch.zeros_like(p)  # persistent bf16 grads: the in-place accumulation modes
+        xs = []
+        for dy in dys:
+            x = x0.clone().requires_grad_(True)
+            h = x
+            for p in params:
+                h = ops.rms_norm(h, p, 1e-5)
+            h.backward(dy)
+            xs.append(x.grad)
+        torch.cuda.synchronize()
+        assert not ops._NORM_PENDING, "a chained dw reduction was left pending after backward"
+        return [p.grad.float().cpu() for p in params], [g.float().cpu() for g in xs]
+
+    g_chain, dx_chain = run(True)
+    g_plain, dx_plain = run(False)
+    for a, b in zip(dx_chain, dx_plain):
+        assert torch.equal(a, b)  # the data path is untouched
+    for a, b in zip(g_chain, g_plain):
+        assert max_abs(a, b) <= _ulp_bound(b.double(), 1), max_abs(a, b)
+    # fp64 restatement of the stack's weight gradients, summed over the two passes
+    ref = [torch.zeros(cols, dtype=torch.float64) for _ in range(3)]
+    for dy in dys:
+        hs = [x0.cpu().double()]
+        for w in ws[:-1]:
+            hs.append(H.rmsnorm_fused(hs[-1].to(BF).double(), w.cpu().double(), 1e-5)[0].to(BF).double())
+        g = dy.cpu().double()
+        for i in (2, 1, 0):
+            dxi, dwi = H.rmsnorm_grads(hs[i].to(BF), ws[i].cpu(), 1e-5, g)
+            ref[i] += dwi.double()
+            g = dxi.to(BF).double()
+    for a, r in zip(g_chain, ref):
+        assert rel_l2(a, r) < 1e-2
+
+
 def test_rmsnorm_residual_prenorm():
     ops = _ops()
     torch.manual_seed(1)
