@@ -492,7 +492,8 @@ _SIDE = {}
 
 def dgrad_wgrad(tag, dy2, W, params, x2):
     """(dx, wgrad_accumulate(...)) for one projection; concurrently on two streams when `tag` is enabled
-    (joined before returning: everything after the projection's backward sees both results)."""
+    (joined before returning: everything after the projection's backward sees both results). Joining later
+    (the next projection's backward) measured the same: the fork / join edges cost ≈ 6 + 11 µs either way."""
     if tag in _conc_tags() and dy2.is_cuda:
         dev = dy2.device
         cur = torch.cuda.current_stream(dev)

@@ -23,23 +23,40 @@ class AdamW(torch.optim.Optimizer):
         defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, amsgrad=False, maximize=False,
                         foreach=None, capturable=False, differentiable=False, fused=fused)
         super().__init__(params, defaults)
-        self._tables = {}  # (group index, step) -> [key, tensors_dev, sizes_dev, chunks_dev, n_chunks, pinned table, event]
+        # per (group, parameter set): device tables of sizes / 64 Ki-element chunks (fixed for the set) and of
+        # the (param, grad, exp_avg, exp_avg_sq) pointers, re-uploaded only when a pointer changed (persistent
+        # gradients: never after the first step); two pinned staging buffers used in turn
+        self._tables = {}
 
-    def _group_tables(self, gi, step, params):
-        chunk = int(_lib.load().pico_adamw_chunk_elems())
-        key = tuple((p.data_ptr(), p.numel()) for p in params)
-        ent = self._tables.get((gi, step))
-        if ent is None or ent[0] != key:
-            sizes = torch.tensor([p.numel() for p in params], dtype=torch.int64)
-            chunks = [(i, c) for i, p in enumerate(params) for c in range(0, p.numel(), chunk)]
+    def _group_tables(self, gi, params):
+        key = (gi, tuple(p.data_ptr() for p in params))
+        ent = self._tables.get(key)
+        if ent is None:
+            chunk = int(_lib.load().pico_adamw_chunk_elems())
             dev = params[0].device
-            chunks_t = torch.tensor(chunks, dtype=torch.int64).reshape(-1, 2)
-            host = torch.empty((len(params), 4), dtype=torch.int64).pin_memory()
-            ent = [key, torch.empty((len(params), 4), dtype=torch.int64, device=dev), sizes.to(dev),
-                   chunks_t.to(dev), len(chunks), host, None]
-            if len(self._tables) > 64:  # step counts keep changing (params joining late): keep the map small
+            sizes = torch.tensor([p.numel() for p in params], dtype=torch.int64)
+            chunks = torch.tensor([(i, c) for i, p in enumerate(params) for c in range(0, p.numel(), chunk)],
+                                  dtype=torch.int64).reshape(-1, 2)
+            ent = {"tens": torch.empty((len(params), 4), dtype=torch.int64, device=dev), "sizes": sizes.to(dev),
+                   "chunks": chunks.to(dev), "n_chunks": chunks.shape[0], "ptrs": None, "turn": 0,
+                   "host": [torch.empty((len(params), 4), dtype=torch.int64).pin_memory() for _ in range(2)],
+                   "done": [None, None]}
+            if len(self._tables) > 64:  # parameter sets keep changing (step counts diverging): keep the map small
                 self._tables.clear()
-            self._tables[(gi, step)] = ent
+            self._tables[key] = ent
+        ptrs = [(p.data_ptr(), p.grad.data_ptr(), self.state[p]["exp_avg"].data_ptr(),
+                 self.state[p]["exp_avg_sq"].data_ptr()) for p in params]
+        if ptrs != ent["ptrs"]:
+            i = ent["turn"]
+            if ent["done"][i] is not None:  # this staging buffer may still be feeding its previous copy
+                ent["done"][i].synchronize()
+            ent["host"][i].numpy()[:] = ptrs
+            ent["tens"].copy_(ent["host"][i], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(params[0].device))
+            ent["done"][i] = ev
+            ent["turn"] = 1 - i
+            ent["ptrs"] = ptrs
         return ent
 
     @torch.no_grad()
@@ -77,17 +94,9 @@ class AdamW(torch.optim.Optimizer):
                 by_step.setdefault(int(st["step"].item()), []).append(p)
             beta1, beta2 = group["betas"]
             for step, ps in sorted(by_step.items()):
-                ent = self._group_tables(gi, step, ps)
-                _, tens, sizes, chunks, n_chunks, host, done = ent
-                if done is not None:  # the pinned table may still be feeding this entry's previous copy
-                    done.synchronize()
-                host.numpy()[:] = [(p.data_ptr(), p.grad.data_ptr(), self.state[p]["exp_avg"].data_ptr(),
-                                    self.state[p]["exp_avg_sq"].data_ptr()) for p in ps]
-                tens.copy_(host, non_blocking=True)
-                ent[6] = torch.cuda.Event()
-                ent[6].record(torch.cuda.current_stream(ps[0].device))
-                _lib.check(lib.pico_adamw_bf16(_lib.ptr(tens), _lib.ptr(sizes), _lib.ptr(chunks), n_chunks,
-                                               float(group["lr"]), float(beta1), float(beta2), float(group["eps"]),
-                                               float(group["weight_decay"]), step, _lib.stream_of(ps[0])),
-                           "pico_adamw_bf16")
+                ent = self._group_tables(gi, ps)
+                _lib.check(lib.pico_adamw_bf16(_lib.ptr(ent["tens"]), _lib.ptr(ent["sizes"]), _lib.ptr(ent["chunks"]),
+                                               ent["n_chunks"], float(group["lr"]), float(beta1), float(beta2),
+                                               float(group["eps"]), float(group["weight_decay"]), step,
+                                               _lib.stream_of(ps[0])), "pico_adamw_bf16")
         return loss
