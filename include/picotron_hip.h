@@ -249,6 +249,14 @@ int pico_cross_entropy_fwd(const void* logits, int64_t ld, const int64_t* target
 int pico_cross_entropy_fwd_grad(void* logits, int64_t ld, const int64_t* target, float* lse, float* loss,
                                 const float* grad_scale, int64_t rows, int64_t vocab, int64_t ignore_index,
                                 void* stream);
+/* The mean's scalars around pico_cross_entropy_fwd_grad, one launch each (instead of the ATen scalar ops of
+ * F.cross_entropy(reduction='mean')'s host code): pico_ce_count writes stats[0] = #(target != ignore_index),
+ * stats[1] = grad_scale / stats[0] (pass stats + 1 as fwd_grad's grad_scale); pico_ce_mean writes
+ * grad_scale * sum(loss_rows) / stats[0] to *out (bf16, or fp32 when out_f32), summed in a fixed order. */
+int pico_ce_count(const int64_t* target, int64_t n, int64_t ignore_index, float grad_scale, float* stats,
+                  void* stream);
+int pico_ce_mean(const float* loss_rows, int64_t n, const float* stats, float grad_scale, void* out, int out_f32,
+                 void* stream);
 int pico_cross_entropy_bwd(const void* logits, int64_t ld, const int64_t* target, const float* lse,
                            const float* grad_scale, void* dlogits, int64_t ldd, int64_t rows, int64_t vocab,
                            int64_t ignore_index, void* stream);

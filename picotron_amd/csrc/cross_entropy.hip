@@ -249,3 +249,65 @@ extern "C" int pico_cross_entropy_bwd(const void* logits, int64_t ld, const int6
                                                                         ignore_index)))
   return 0;
 }
+
+// ---------------------------------------------------------------------------------------------------
+// The mean's scalar bookkeeping around the fused LM-head CE (ref train.py:46-49, reduction='mean'), one
+// 1024-thread workgroup each instead of ~9 ATen scalar launches per micro-batch:
+//   pico_ce_count: stats[0] = number of targets != ignore_index, stats[1] = grad_scale / stats[0]
+//     (the per-row gradient scale pico_cross_entropy_fwd_grad reads);
+//   pico_ce_mean: out (bf16, or fp32 when out_f32) = grad_scale * sum(loss_rows) / stats[0],
+//     summed in a fixed order (deterministic).
+namespace {
+constexpr int CE_NT = 1024;
+
+PICO_DEV float block_sum_1024(float v, float* red) {
+  v = wave_sum_dpp(v);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  float t = 0.f;
+  if (threadIdx.x == 0)
+    for (int w = 0; w < CE_NT / 64; ++w) t += red[w];  // waves in order
+  return t;
+}
+
+__global__ __launch_bounds__(CE_NT) void ce_count_kernel(const int64_t* __restrict__ target, int64_t n,
+                                                         int64_t ignore_index, float grad_scale, float* stats) {
+  __shared__ float red[CE_NT / 64];
+  float c = 0.f;
+  for (int64_t i = threadIdx.x; i < n; i += CE_NT) c += target[i] != ignore_index ? 1.f : 0.f;
+  const float t = block_sum_1024(c, red);  // exact: integer counts below 2^24
+  if (threadIdx.x == 0) {
+    stats[0] = t;
+    stats[1] = grad_scale / t;
+  }
+}
+
+__global__ __launch_bounds__(CE_NT) void ce_mean_kernel(const float* __restrict__ loss_rows, int64_t n,
+                                                        const float* __restrict__ stats, float grad_scale, void* out,
+                                                        int out_f32) {
+  __shared__ float red[CE_NT / 64];
+  float s = 0.f;
+  for (int64_t i = threadIdx.x; i < n; i += CE_NT) s += loss_rows[i];
+  const float t = block_sum_1024(s, red);
+  if (threadIdx.x == 0) {
+    const float v = t / stats[0] * grad_scale;
+    if (out_f32) *(float*)out = v;
+    else *(bf16_t*)out = f2bf(v);
+  }
+}
+}  // namespace
+
+extern "C" int pico_ce_count(const int64_t* target, int64_t n, int64_t ignore_index, float grad_scale, float* stats,
+                             void* stream) {
+  PICO_REQUIRE(target && stats && n >= 0, "pico_ce_count: bad arguments");
+  PICO_TRY(pico_launch(PICO_K_CE_FWD, "ce_count", ce_count_kernel, dim3(1), dim3(CE_NT), 0, (hipStream_t)stream, target, n, ignore_index, grad_scale, stats));
+  return 0;
+}
+
+extern "C" int pico_ce_mean(const float* loss_rows, int64_t n, const float* stats, float grad_scale, void* out,
+                            int out_f32, void* stream) {
+  PICO_REQUIRE(loss_rows && stats && out && n >= 0, "pico_ce_mean: bad arguments");
+  PICO_TRY(pico_launch(PICO_K_CE_FWD, "ce_mean", ce_mean_kernel, dim3(1), dim3(CE_NT), 0, (hipStream_t)stream, loss_rows, n, stats, grad_scale, out, out_f32));
+  return 0;
+}

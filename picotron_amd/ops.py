@@ -681,8 +681,11 @@ class _LMHeadCEChunkedFn(torch.autograd.Function):
         if t.dtype != torch.int64:
             t = t.long()
         t = t.contiguous()
-        n_valid = (t != ignore_index).sum().to(torch.float32)
-        gscale = (float(grad_scale) / n_valid).reshape(1)
+        # [n_valid, grad_scale / n_valid] in one launch (pico_ce_count)
+        stats = torch.empty(2, dtype=torch.float32, device=x.device)
+        _lib.check(_lib.load().pico_ce_count(_lib.ptr(t), T, int(ignore_index), float(grad_scale), _lib.ptr(stats),
+                                             _lib.stream_of(x)), "pico_ce_count")
+        gscale = stats[1:]
         lse = torch.empty(T, dtype=torch.float32, device=x.device)
         loss_rows = torch.empty(T, dtype=torch.float32, device=x.device)
         dx = torch.empty(T, H, dtype=x.dtype, device=x.device)
@@ -745,12 +748,14 @@ class _LMHeadCEChunkedFn(torch.autograd.Function):
                     torch.mm(lg, w, out=dx[c0:c1])
             if side is not None:
                 torch.cuda.current_stream(x.device).wait_stream(side)
-        loss = loss_rows.sum() / n_valid * grad_scale
+        loss = torch.empty((), dtype=x.dtype, device=x.device)
+        _lib.check(lib.pico_ce_mean(_lib.ptr(loss_rows), T, _lib.ptr(stats), float(grad_scale), _lib.ptr(loss),
+                                    1 if x.dtype == torch.float32 else 0, _lib.stream_of(x)), "pico_ce_mean")
         ctx.save_for_backward(dx)
         ctx.xshape = x.shape
         ctx.dw = dst if kind == "autograd_acc" else None
         ctx.ready = ready
-        return loss.to(x.dtype)
+        return loss
 
     @staticmethod
     def backward(ctx, grad_out):
