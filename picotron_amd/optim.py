@@ -59,6 +59,23 @@ class AdamW(torch.optim.Optimizer):
             ent["ptrs"] = ptrs
         return ent
 
+    def zero_grad(self, set_to_none=True):
+        """torch.optim.Optimizer.zero_grad; zeroing in place (set_to_none=False: persistent gradient buffers,
+        as HIP-graph replay needs) runs as multi-tensor launches instead of one launch per parameter."""
+        if set_to_none:
+            return super().zero_grad(set_to_none=True)
+        grads = []
+        for group in self.param_groups:
+            for p in group["params"]:
+                if p.grad is not None:
+                    if p.grad.grad_fn is not None:
+                        p.grad.detach_()
+                    else:
+                        p.grad.requires_grad_(False)
+                    grads.append(p.grad)
+        if grads:
+            torch._foreach_zero_(grads)
+
     @torch.no_grad()
     def step(self, closure=None):
         loss = None
