@@ -78,7 +78,8 @@ def kernel_work(kid, cfg, mbs, seq):
         # rstd, small dw partials)
         L.K_RMSNORM_FWD: (5 * T * Hd * 2 + 4 * T, "byte", "hbm"),
         L.K_RMSNORM_BWD: (4 * T * Hd * 2 + 4 * T, "byte", "hbm"),
-        L.K_ROPE: (2 * T * (H + Hkv) * D * 2, "byte", "hbm"),  # q|k heads in one launch, read + write
+        # k heads (q is rotated inside the attention forward), read + write; q|k with PICO_FUSE_ROPE_Q=0
+        L.K_ROPE: (2 * T * (Hkv + (H if os.getenv("PICO_FUSE_ROPE_Q", "1") == "0" else 0)) * D * 2, "byte", "hbm"),
         L.K_SWIGLU_FWD: (4 * T * I * 2, "byte", "hbm"),  # g, u read; h and h^T written
         L.K_SWIGLU_BWD: (5 * T * I * 2, "byte", "hbm"),
         # reads O, dO, LSE; writes delta and LSE*log2(e) (fp32 per query row and head)

@@ -188,6 +188,10 @@ typedef struct pico_attn_args {
  * are returned rotated back by -theta (the RoPE backward, ref picotron/model.py:135-136), fused into
  * the dQ slab sum and the dK epilogue. Not combinable with PICO_ATTN_DQ_F32_ACCUM. */
 #define PICO_ATTN_ROPE_BWD 2
+/* fwd: q holds UNROTATED queries; each row is rotated (RoPE, rotate-half, position = sequence index,
+ * tables as for ROPE_BWD) in registers before use, and the rotated rows are written to dq (dq_strides;
+ * dq may alias q) for the backward. Replaces the query half of the separate pico_rope launch. */
+#define PICO_ATTN_ROPE_Q_FWD 4
 
 int64_t pico_attn_args_size(void); /* sizeof(pico_attn_args), for FFI layout checks */
 int pico_attn_fwd(const pico_attn_args* args, void* stream);

@@ -30,6 +30,7 @@ KERNEL_NAMES = {
 
 ATTN_DQ_F32_ACCUM = 1
 ATTN_ROPE_BWD = 2
+ATTN_ROPE_Q_FWD = 4
 
 c_i64 = ctypes.c_int64
 c_vp = ctypes.c_void_p

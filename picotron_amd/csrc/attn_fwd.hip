@@ -164,6 +164,24 @@ __attribute__((amdgpu_waves_per_eu(FwdCfg<D>::WAVES_PER_EU, FwdCfg<D>::WAVES_PER
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) qf[ks] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u16x8*>(qp + 16 * ks));
   }
+  // PICO_ATTN_ROPE_Q_FWD: q holds the unrotated rows. The rotate-half pairs (d, d + D/2) sit in the
+  // same lane (k-steps ks and ks + KS/2), so the rotation happens in registers, with the rope
+  // kernel's arithmetic (fp32, one rounding). The tables load beside q; the rotation runs after the
+  // first K/V tiles are issued, and the rotated row (still in qf) is stored to dq in the epilogue, so
+  // neither sits in the vmcnt queue ahead of the first tiles. Each query row is loaded by exactly one
+  // lane of one workgroup, so dq may alias q.
+  const bool rope_q = (a.flags & PICO_ATTN_ROPE_Q_FWD) != 0;
+  u16x8 rc[KS / 2], rs[KS / 2];
+  if (rope_q) {
+    const int pos = min(my_q, Sq - 1);
+    const bf16_t* cp = (const bf16_t*)a.rope_cos + (int64_t)pos * a.rope_stride + 8 * h;
+    const bf16_t* sp = (const bf16_t*)a.rope_sin + (int64_t)pos * a.rope_stride + 8 * h;
+#pragma unroll
+    for (int ks = 0; ks < KS / 2; ++ks) {
+      rc[ks] = *reinterpret_cast<const u16x8*>(cp + 16 * ks);
+      rs[ks] = *reinterpret_cast<const u16x8*>(sp + 16 * ks);
+    }
+  }
 
   // tiles this workgroup visits; the last key any of its rows may see is `wg_lim`
   int kend = Sk;
@@ -363,6 +381,22 @@ __attribute__((amdgpu_waves_per_eu(FwdCfg<D>::WAVES_PER_EU, FwdCfg<D>::WAVES_PER
 #pragma unroll
   for (int t = 0; t < P; ++t)
     if (t < ntiles) issue(t);
+  if (rope_q) {
+#pragma unroll
+    for (int ks = 0; ks < KS / 2; ++ks) {
+      const u16x8 x1 = __builtin_bit_cast(u16x8, qf[ks]), x2 = __builtin_bit_cast(u16x8, qf[ks + KS / 2]);
+      u16x8 o1, o2;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float xa = bf2f(x1[j]), xb = bf2f(x2[j]);
+        const float cf = bf2f(rc[ks][j]), sf = bf2f(rs[ks][j]);
+        o1[j] = f2bf(xa * cf - xb * sf);
+        o2[j] = f2bf(xb * cf + xa * sf);
+      }
+      qf[ks] = __builtin_bit_cast(bf16x8, o1);
+      qf[ks + KS / 2] = __builtin_bit_cast(bf16x8, o2);
+    }
+  }
 
 #if PICO_FWD_WGSTAMP
   wgs[1] = __builtin_amdgcn_s_memrealtime();
@@ -402,6 +436,11 @@ __attribute__((amdgpu_waves_per_eu(FwdCfg<D>::WAVES_PER_EU, FwdCfg<D>::WAVES_PER
   {
     bf16_t* op = (bf16_t*)a.o + b * a.o_strides[0] + hq * a.o_strides[2] + (int64_t)min(my_q, Sq - 1) * a.o_strides[1];
     store_row_bf16_x16<DT>(op, h, row_ok, [&](int dt, int i) { return o[dt][i] * inv; });
+  }
+  if (rope_q && row_ok) {  // the rotated q row, for the backward
+    bf16_t* rq = (bf16_t*)a.dq + b * a.dq_strides[0] + hq * a.dq_strides[2] + (int64_t)my_q * a.dq_strides[1] + 8 * h;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) *reinterpret_cast<u16x8*>(rq + 16 * ks) = __builtin_bit_cast(u16x8, qf[ks]);
   }
   if (a.o_t) {  // uniform: O^T [Hq*D][tokens]
     constexpr int TP = BM + 8;  // pitch (elements) of the transposed staging tile
@@ -468,6 +507,15 @@ extern "C" int pico_attn_fwd(const pico_attn_args* a, void* stream) {
   if (rc) return rc;
   PICO_REQUIRE(a->o && a->lse, "pico_attn_fwd: null output");
   PICO_REQUIRE(!a->o_t || a->o_t_ld >= a->batch * a->seqlen_q, "pico_attn_fwd: o_t_ld must cover the tokens");
+  if (a->flags & PICO_ATTN_ROPE_Q_FWD) {
+    PICO_REQUIRE(a->dq && a->rope_cos && a->rope_sin, "pico_attn_fwd: ROPE_Q_FWD needs dq and the cos/sin tables");
+    PICO_REQUIRE(((uintptr_t)a->dq | (uintptr_t)a->rope_cos | (uintptr_t)a->rope_sin) % 16 == 0,
+                 "pico_attn_fwd: ROPE_Q_FWD needs 16-byte aligned dq and tables");
+    PICO_REQUIRE(a->rope_stride % 8 == 0 && a->rope_stride >= a->head_dim / 2,
+                 "pico_attn_fwd: bad rope table row stride %lld", (long long)a->rope_stride);
+    for (int d = 0; d < 3; ++d)
+      PICO_REQUIRE(a->dq_strides[d] % 8 == 0, "pico_attn_fwd: dq strides must be multiples of 8 elements");
+  }
   if (a->batch == 0 || a->seqlen_q == 0 || a->heads_q == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   if (a->head_dim == 64) return launch_fwd<64>(a, s);

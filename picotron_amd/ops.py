@@ -944,10 +944,15 @@ def _check_qkv(q, k, v):
         raise ValueError("flash attention: heads_q must be a multiple of heads_kv")
 
 
-def attention_block_fwd(q, k, v, softmax_scale, causal, o_t=None):
+def attention_block_fwd(q, k, v, softmax_scale, causal, o_t=None, rope_q=None):
     """O [B,Sq,Hq,D] bf16 and LSE [B,Hq,Sq] fp32 (natural log) of softmax(scale*QK^T [+causal]) V.
-    o_t (optional, bf16 [Hq*D, >= B*Sq] with unit column stride) also receives O transposed."""
+    o_t (optional, bf16 [Hq*D, >= B*Sq] with unit column stride) also receives O transposed.
+    rope_q = (cos, sin) ([>= S, D/2] bf16 tables): q is UNROTATED; the kernel applies RoPE to it in
+    registers and writes the rotated queries back into q in place (PICO_ATTN_ROPE_Q_FWD)."""
     _check_qkv(q, k, v)
+    if rope_q is not None and (q.stride(-1) != 1 or any(s % 8 for s in q.stride()[:3])):
+        raise ValueError("attention_block_fwd: rope_q rotates q in place; q needs unit last stride and "
+                         "strides that are multiples of 8")
     q, k, v = [t if t.stride(-1) == 1 and all(s % 8 == 0 for s in t.stride()[:3]) else t.contiguous()
                for t in (q, k, v)]
     B, Sq, Hq, D = q.shape
@@ -959,6 +964,12 @@ def attention_block_fwd(q, k, v, softmax_scale, causal, o_t=None):
         if o_t.shape[0] != Hq * D or o_t.stride(1) != 1 or o_t.shape[1] < B * Sq:
             raise ValueError("attention_block_fwd: o_t must be [Hq*D, >= B*Sq] with unit column stride")
         a.o_t, a.o_t_ld = _lib.ptr(o_t), o_t.stride(0)
+    if rope_q is not None:
+        cos, sin = rope_q
+        _check_rope_tables(cos, sin, D)
+        a.flags |= _lib.ATTN_ROPE_Q_FWD
+        a.rope_cos, a.rope_sin, a.rope_stride = _lib.ptr(cos), _lib.ptr(sin), cos.stride(0)
+        a.dq, a.dq_strides = _lib.ptr(q), _lib.i64x3(q.stride()[:3])
     _lib.check(_lib.load().pico_attn_fwd(ctypes.byref(a), _lib.stream_of(q)), "pico_attn_fwd")
     return o, lse
 
@@ -1024,8 +1035,8 @@ def flash_attn_func(q, k, v, dropout_p=0.0, softmax_scale=None, causal=False, wi
 
 class _QKVRopeAttentionFn(torch.autograd.Function):
     """The attention block's hot path in one autograd node:
-      qkv = x [Wq; Wk; Wv]^T (ONE GEMM) -> RoPE in place on the q|k columns (ONE launch, q and k heads
-      are adjacent in qkv) -> flash attention reading q/k/v as strided views of qkv.
+      qkv = x [Wq; Wk; Wv]^T (ONE GEMM) -> RoPE in place on the k columns (one launch) -> flash attention
+      reading q/k/v as strided views of qkv, rotating q in registers and storing it back into qkv.
     Backward: attention writes dq/dk/dv straight into the column blocks of one dqkv buffer with RoPE^-1
     applied inside it (dQ slab sum, dK epilogue), then dx = dqkv W (one GEMM, no sum of three dgrads) and
     dW = dqkv^T x (one GEMM, rows = dWq | dWk | dWv)."""
@@ -1039,15 +1050,18 @@ class _QKVRopeAttentionFn(torch.autograd.Function):
         N = W.shape[0]
         x2 = x.reshape(B * S, Hd)
         qkv = torch.matmul(x2, W.t())  # [T, (nh + 2 nkv) D]
-        qk = qkv.view(B, S, N // D, D)[:, :, : nh + nkv]  # q|k heads, row stride N
-        _rope_launch(qk, qk, cos, sin, False)
         heads = qkv.view(B, S, N // D, D)
         q, k, v = heads[:, :, :nh], heads[:, :, nh:nh + nkv], heads[:, :, nh + nkv:]
+        # RoPE: k in place by the rope kernel; q inside the attention forward, which writes the rotated
+        # q back into qkv for the backward (PICO_FUSE_ROPE_Q=0: q|k in one rope launch, for A/B)
+        fuse_q = os.getenv("PICO_FUSE_ROPE_Q", "1") != "0"
+        qk = k if fuse_q else heads[:, :, : nh + nkv]  # row stride N
+        _rope_launch(qk, qk, cos, sin, False)
         scale = 1.0 / math.sqrt(D)
         # O^T for the out-projection's wgrad (TT form), written by the attention epilogue for free
         o_t = torch.empty((nh * D, B * S), dtype=x.dtype, device=x.device) \
             if os.getenv("PICO_XT_WGRAD", "1") != "0" else None
-        o, lse = attention_block_fwd(q, k, v, scale, causal, o_t=o_t)
+        o, lse = attention_block_fwd(q, k, v, scale, causal, o_t=o_t, rope_q=(cos, sin) if fuse_q else None)
         ctx.save_for_backward(_wgrad_input(x2, N, x), W, qkv, o, lse, cos, sin)
         ctx.params = (wq, wk, wv)
         ctx.meta = (B, S, Hd, nh, nkv, D, causal, scale)
@@ -1085,6 +1099,13 @@ def qkv_rope_attention(x, wq, wk, wv, cos, sin, num_heads, num_kv_heads, causal)
                                      causal)
 
 
+def _check_rope_tables(cos, sin, D):
+    _need(cos, "cos")
+    _need(sin, "sin")
+    if cos.stride(1) != 1 or sin.stride(1) != 1 or sin.stride(0) != cos.stride(0) or cos.shape[1] * 2 != D:
+        raise ValueError("attention rope: cos/sin must be [>= S, D/2] with unit column stride")
+
+
 def _attention_bwd_into(dout, q, k, v, o, lse, softmax_scale, causal, dq, dk, dv, rope=None):
     """attention backward writing into caller-provided (possibly strided) dq/dk/dv. rope = (cos, sin)
     ([>= S, D/2] bf16 tables): q and k were rotated before the forward; dq and dk come back rotated by
@@ -1100,10 +1121,7 @@ def _attention_bwd_into(dout, q, k, v, o, lse, softmax_scale, causal, dq, dk, dv
     a.dv_strides = _lib.i64x3(dv.stride()[:3])
     if rope is not None:
         cos, sin = rope
-        _need(cos, "cos")
-        _need(sin, "sin")
-        if cos.stride(1) != 1 or sin.stride(0) != cos.stride(0) or cos.shape[1] * 2 != q.shape[3]:
-            raise ValueError("attention rope backward: cos/sin must be [>= S, D/2] with unit column stride")
+        _check_rope_tables(cos, sin, q.shape[3])
         a.flags |= _lib.ATTN_ROPE_BWD
         a.rope_cos, a.rope_sin, a.rope_stride = _lib.ptr(cos), _lib.ptr(sin), cos.stride(0)
     lib = _lib.load()

@@ -688,6 +688,38 @@ def test_attention_rope_bwd_fused(B, S, Hq, Hkv, D):
     assert rel_l2(dk.float().cpu(), ref_dk.float().cpu()) < 4e-3
 
 
+@pytest.mark.parametrize("B,S,Hq,Hkv,D,causal", [(4, 1024, 32, 32, 64, True), (2, 200, 4, 2, 64, True),
+                                                  (1, 384, 4, 4, 128, True), (1, 330, 4, 2, 128, False)])
+def test_attention_rope_q_fwd_fused(B, S, Hq, Hkv, D, causal):
+    """PICO_ATTN_ROPE_Q_FWD (RoPE on q inside the attention forward, rotated q stored back into the qkv
+    buffer) == pico_rope on q followed by the plain forward: the stored q within one bf16 ulp of the rope
+    kernel's (bit-equal when both round alike, and then O and LSE bit-equal too), k/v columns untouched."""
+    from picotron_amd import ops
+    from picotron_amd.model import get_cos_sin
+    torch.manual_seed(S + D + Hkv)
+    qkv = torch.randn(B, S, Hq + 2 * Hkv, D, dtype=BF, device=DEV)
+    cos, sin = get_cos_sin(S, D, base=10000.0)
+    cos, sin = cos.to(DEV, BF)[:, : D // 2], sin.to(DEV, BF)[:, : D // 2]
+    sc = 1.0 / math.sqrt(D)
+    q0 = qkv[:, :, :Hq]
+    q_ref = torch.empty(q0.shape, dtype=BF, device=DEV)
+    ops._rope_launch(q0, q_ref, cos, sin, False)
+    kv0 = qkv[:, :, Hq:].clone()
+    o_ref, lse_ref = ops.attention_block_fwd(q_ref, qkv[:, :, Hq:Hq + Hkv], qkv[:, :, Hq + Hkv:], sc, causal)
+    o, lse = ops.attention_block_fwd(qkv[:, :, :Hq], qkv[:, :, Hq:Hq + Hkv], qkv[:, :, Hq + Hkv:], sc, causal,
+                                     rope_q=(cos, sin))
+    torch.cuda.synchronize()
+    q = qkv[:, :, :Hq]
+    assert torch.equal(qkv[:, :, Hq:], kv0)
+    ulp = q_ref.float().abs().clamp_min(1e-30) * 2.0 ** -7
+    assert bool(((q.float() - q_ref.float()).abs() <= ulp).all())
+    if torch.equal(q, q_ref):
+        assert torch.equal(o, o_ref) and torch.equal(lse, lse_ref)
+    else:
+        assert rel_l2(o.float().cpu(), o_ref.float().cpu()) < 2e-3
+        assert float((lse - lse_ref).abs().max()) < 1e-2
+
+
 @pytest.mark.parametrize("B,S,H,D,causal", [(2, 256, 4, 64, True), (1, 200, 2, 128, False)])
 def test_attention_fwd_transposed_output(B, S, H, D, causal):
     """pico_attn_fwd's optional o_t output == O transposed to [H*D, tokens], bit for bit (same rounding),
