@@ -735,12 +735,12 @@ def test_attention_fwd_transposed_output(B, S, H, D, causal):
     assert torch.equal(o_t, o.reshape(B * S, H * D).t())
 
 
-def test_swiglu_fwd_transposed_output():
+@pytest.mark.parametrize("T,I", [(256, 512), (192, 576)])  # 128-column tiles; 64-column tiles (I % 128 != 0)
+def test_swiglu_fwd_transposed_output(T, I):
     """pico_swiglu_fwd_t == pico_swiglu_fwd bit for bit on h, and writes h^T exactly (fused gate|up layout)."""
     from picotron_amd import _lib as L
     from picotron_amd import ops
     torch.manual_seed(5)
-    T, I = 256, 512
     gu = torch.randn(T, 2 * I, dtype=BF, device=DEV)
     h_ref = torch.empty(T, I, dtype=BF, device=DEV)
     ops._swiglu_fwd(gu, gu[:, I:], h_ref, T, I, 2 * I, I)
