@@ -89,6 +89,9 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd_kernel(const bf16_t* __restri
 #ifndef PICO_RMS_FWDT_ROWS
 #define PICO_RMS_FWDT_ROWS 16
 #endif
+#ifndef PICO_RMS_FWDT_QUAD
+#define PICO_RMS_FWDT_QUAD 1
+#endif
 constexpr int FWDT_WAVES = PICO_RMS_FWDT_WAVES;  // waves per tile (rows per wave = FWDT_ROWS / FWDT_WAVES)
 constexpr int FWDT_ROWS = PICO_RMS_FWDT_ROWS;
 static_assert(FWDT_ROWS == 16 || FWDT_ROWS == 32, "tile rows");
@@ -102,7 +105,13 @@ __global__ __launch_bounds__(FWDT_WAVES * 64) void rmsnorm_fwd_t_kernel(const bf
   extern __shared__ __attribute__((aligned(16))) unsigned short tile[];  // [FWDT_ROWS][PITCH]
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   int64_t tidx = blockIdx.x;
-  if (FWDT_ROWS == 16 && (gridDim.x & 15) == 0) {  // blocks b, b + 8 (one XCD): tile pair (2p, 2p + 1) of one y^T line
+  if (FWDT_ROWS == 16 && PICO_RMS_FWDT_QUAD && (gridDim.x & 31) == 0) {
+    // blocks b, b + 8, b + 16, b + 24 (one XCD): the four tiles (4p .. 4p + 3) whose 32-byte y^T segments
+    // make one 128-byte line
+    const int64_t b = blockIdx.x, g = b >> 5;
+    const int xcd = (int)(b & 7), q = (int)((b >> 3) & 3);
+    tidx = 4 * (g * 8 + xcd) + q;
+  } else if (FWDT_ROWS == 16 && (gridDim.x & 15) == 0) {  // blocks b, b + 8 (one XCD): tile pair (2p, 2p + 1)
     const int64_t b = blockIdx.x, g = b >> 4;
     const int xcd = (int)(b & 7), half = (int)((b >> 3) & 1);
     tidx = 2 * (g * 8 + xcd) + half;

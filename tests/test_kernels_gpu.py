@@ -754,7 +754,7 @@ def test_swiglu_fwd_transposed_output(T, I):
     assert bool((ht[:, T:] == 2.0).all())
 
 
-@pytest.mark.parametrize("rows,cols,res", [(64, 2048, True), (96, 1024, False), (4096, 2048, True)])
+@pytest.mark.parametrize("rows,cols,res", [(64, 2048, True), (96, 1024, False), (256, 2048, True), (4096, 2048, True)])
 def test_rmsnorm_fwd_transposed_output(rows, cols, res):
     """pico_rmsnorm_fwd_t == pico_rmsnorm_fwd bit for bit (y, residual_out, rstd) and writes y^T exactly."""
     from picotron_amd import ops
