@@ -261,6 +261,11 @@ int pico_ce_count(const int64_t* target, int64_t n, int64_t ignore_index, float 
                   void* stream);
 int pico_ce_mean(const float* loss_rows, int64_t n, const float* stats, float grad_scale, void* out, int out_f32,
                  void* stream);
+/* backward of the fused LM-head CE: dx (bf16, contiguous, n elements) *= *upstream (the loss's upstream
+ * gradient, a device 0-dim bf16 tensor, or fp32 when upstream_f32, rounded to bf16 first as ATen does),
+ * fp32 product, one bf16 rounding.
+ * Replaces autograd's scaling of the reference's logits gradient (ref picotron/model.py:269, train.py:46-49). */
+int pico_ce_scale_grad(void* dx, int64_t n, const void* upstream, int upstream_f32, void* stream);
 int pico_cross_entropy_bwd(const void* logits, int64_t ld, const int64_t* target, const float* lse,
                            const float* grad_scale, void* dlogits, int64_t ldd, int64_t rows, int64_t vocab,
                            int64_t ignore_index, void* stream);

@@ -645,15 +645,25 @@ class _LMHeadCEFn(torch.autograd.Function):
         g = grad_out.to(torch.float32)
         dx = None
         if ctx.needs_input_grad[0]:
-            dx = dgrad(dlogits, w, (w,))
-            dx.mul_(g)
-            dx = dx.view(ctx.xshape)
+            dx = _scale_by_upstream(dgrad(dlogits, w, (w,)), grad_out).view(ctx.xshape)
         dw = None
         if ctx.needs_input_grad[1]:
             # scale the small GEMM input instead of dlogits: dW = dlogits^T (g x) (layout of x^T kept;
             # exact when g is a power of two, e.g. 1 / grad_acc)
             dw = wgrad_accumulate((w,), dlogits, xin * g)[0]
         return dx, dw, None, None
+
+
+def _scale_by_upstream(dx, grad_out):
+    """dx (bf16, contiguous) *= the loss's upstream gradient, read on the device (pico_ce_scale_grad: same
+    rounding as ATen's dx.mul_(grad_out), one streaming launch instead of a cast + a broadcasting ATen mul)."""
+    if dx.dtype != torch.bfloat16 or not dx.is_contiguous() or grad_out.dtype not in (torch.bfloat16, torch.float32):
+        return dx.mul_(grad_out.to(torch.float32))
+    g = grad_out if grad_out.is_contiguous() else grad_out.contiguous()
+    _lib.check(_lib.load().pico_ce_scale_grad(_lib.ptr(dx), dx.numel(), _lib.ptr(g),
+                                              1 if g.dtype == torch.float32 else 0, _lib.stream_of(dx)),
+               "pico_ce_scale_grad")
+    return dx
 
 
 class _LMHeadCEChunkedFn(torch.autograd.Function):
@@ -760,12 +770,11 @@ class _LMHeadCEChunkedFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, grad_out):
         (dx,) = ctx.saved_tensors
-        g = grad_out.to(torch.float32)
         if os.getenv("PICO_CHECK_GRAD_SCALE", "0") == "1":
-            assert float(g) == 1.0, f"lm_head_cross_entropy(grad_scale=...): upstream gradient {float(g)} != 1"
+            assert float(grad_out) == 1.0, f"lm_head_cross_entropy(grad_scale=...): upstream gradient {float(grad_out)} != 1"
         dxo = None
         if ctx.needs_input_grad[0]:
-            dxo = dx.mul_(g).view(ctx.xshape)
+            dxo = _scale_by_upstream(dx, grad_out).view(ctx.xshape)
         if ctx.ready is not None:
             ctx.ready()
         dw = ctx.dw

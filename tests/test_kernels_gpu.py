@@ -596,6 +596,23 @@ def test_lm_head_cross_entropy_fused(V, ignore, g):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n,gdt,g", [(4096 * 2048, torch.bfloat16, 1.0), (1000, torch.float32, 0.37),
+                                     (8 * 257 + 5, torch.bfloat16, 1.0 / 3), (3, torch.float32, -2.5)])
+def test_ce_scale_grad_matches_torch_mul(n, gdt, g):
+    """pico_ce_scale_grad (the LM-head CE backward's dx *= upstream gradient, read on the device) == ATen's
+    dx.mul_(upstream) bit for bit (ATen casts the 0-dim operand to bf16 first), vector body and scalar tail."""
+    from picotron_amd import ops
+    torch.manual_seed(n)
+    dx = torch.randn(n, dtype=BF, device=DEV)
+    up = torch.tensor(g, dtype=gdt, device=DEV)
+    ref = dx.clone().mul_(up)
+    out = ops._scale_by_upstream(dx, up)
+    torch.cuda.synchronize()
+    assert out.data_ptr() == dx.data_ptr()
+    assert torch.equal(out, ref)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("T,chunk,V,ignore,mode", [(512, 128, 4000, False, "grad"), (500, 192, 4000, True, "fresh"),
                                                    (1024, 1024, 49152, True, "grad"), (700, 256, 4000, True, "autograd"),
                                                    (384, 100, 4000, False, "nograd")])
