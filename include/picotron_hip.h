@@ -199,11 +199,18 @@ int64_t pico_attn_bwd_workspace_bytes(const pico_attn_args* args);
 int pico_attn_bwd(const pico_attn_args* args, void* stream);
 
 /* ---- ring-attention block merge (update_out_and_lse) ----
- * out fp32 [B, S, H, D] contiguous, lse fp32 [B, H, S]; block_out bf16 [B, S, H, D] with element
- * strides (batch, seq, head); block_lse fp32 [B, H, S]. first != 0: out = block_out, lse = block_lse. */
-int pico_attn_merge(float* out, float* lse, const void* block_out, const float* block_lse, int64_t batch,
-                    int64_t seqlen, int64_t heads, int64_t head_dim, const int64_t* block_out_strides, int first,
-                    void* stream);
+ * ref picotron/context_parallel/context_parallel.py:157-187:
+ *   first != 0: out = float(block_out), lse = block_lse
+ *   otherwise:  out -= sigmoid(block_lse - lse) * (out - block_out); lse -= logsigmoid(lse - block_lse)
+ * Every operand by element strides, so the reference's layout (out [B, H, S, D] fp32 and lse [B, H, S, 1],
+ * or slices of them, ref :183-186) and the ring's internal [B, S, H, D] one use the same entry point:
+ * out fp32, strides (batch, seq, head), unit head_dim stride; lse fp32, strides (batch, head, seq);
+ * block_out bf16 (block_out_f32 == 0) or fp32, strides (batch, seq, head), unit head_dim stride;
+ * block_lse fp32, strides (batch, head, seq). out and block_out rows 16-byte aligned. */
+int pico_attn_merge(float* out, const int64_t* out_strides, float* lse, const int64_t* lse_strides,
+                    const void* block_out, const int64_t* block_out_strides, int block_out_f32,
+                    const float* block_lse, const int64_t* block_lse_strides, int64_t batch, int64_t seqlen,
+                    int64_t heads, int64_t head_dim, int first, void* stream);
 
 /* ---- DP gradient buckets ---- */
 /* main_grad[i] = (main_grad[i] + float(grad[i])) * (1.0f / divide_by)   (divide_by == 1: no scaling).

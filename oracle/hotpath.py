@@ -153,14 +153,24 @@ def attention_bwd(dO, q, k, v, O, lse, sm_scale, causal):
     return dQ, dK, dV
 
 
-def update_out_and_lse(out, lse, block_out, block_lse):
-    """ref .../context_parallel.py:157-187 (sigmoid/logsigmoid merge; out fp32, lse [..., 1])."""
+def update_out_and_lse(out, lse, block_out, block_lse, slice_=None):
+    """ref .../context_parallel.py:157-187 (sigmoid/logsigmoid merge; out fp32, lse [..., 1]; slice_ merges
+    into out[slice_] / lse[slice_] only, :183-184)."""
+    def _update(current_out, current_lse):
+        current_out = current_out - F.sigmoid(block_lse - current_lse) * (current_out - block_out)
+        current_lse = current_lse - F.logsigmoid(current_lse - block_lse)
+        return current_out, current_lse
+
     block_out = block_out.to(torch.float32)
     block_lse = block_lse.unsqueeze(dim=-1)
     if out is None:
+        if slice_ is not None:
+            raise RuntimeError("first update_out_and_lse should not pass slice_ args")
         return block_out, block_lse
-    out = out - F.sigmoid(block_lse - lse) * (out - block_out)
-    lse = lse - F.logsigmoid(lse - block_lse)
+    if slice_ is not None:
+        out[slice_], lse[slice_] = _update(out[slice_], lse[slice_])
+    else:
+        out, lse = _update(out, lse)
     return out, lse
 
 

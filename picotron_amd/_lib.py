@@ -77,8 +77,9 @@ _SIGNATURES = {
     "pico_attn_fwd": (ctypes.c_int, [ctypes.POINTER(AttnArgs), c_vp]),
     "pico_attn_bwd_workspace_bytes": (c_i64, [ctypes.POINTER(AttnArgs)]),
     "pico_attn_bwd": (ctypes.c_int, [ctypes.POINTER(AttnArgs), c_vp]),
-    "pico_attn_merge": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64,
-                                       ctypes.POINTER(c_i64), ctypes.c_int, c_vp]),
+    "pico_attn_merge": (ctypes.c_int, [c_vp, ctypes.POINTER(c_i64), c_vp, ctypes.POINTER(c_i64), c_vp,
+                                       ctypes.POINTER(c_i64), ctypes.c_int, c_vp, ctypes.POINTER(c_i64), c_i64, c_i64,
+                                       c_i64, c_i64, ctypes.c_int, c_vp]),
     "pico_grad_accum": (ctypes.c_int, [c_vp, c_vp, c_i64, ctypes.c_float, c_vp]),
     "pico_scale_f32": (ctypes.c_int, [c_vp, c_i64, ctypes.c_float, c_vp]),
     "pico_cast_f32_bf16": (ctypes.c_int, [c_vp, c_vp, c_i64, c_vp]),

@@ -30,9 +30,17 @@ from .cp_communications import ContextCommunicate
 
 
 def apply_context_parallel(model, zigzag=None):
+    """ref :10-12 (sets CONTEXT_PARALLEL). zigzag=True/False also switches the sequence layout; the decoder
+    layers' RoPE tables, sliced when the model was built, are re-sliced for the layout now in force, so the
+    reference's order (build the model, then apply CP, ref train.py:175-188) rotates every rank's rows by
+    their global positions."""
     os.environ["CONTEXT_PARALLEL"] = "1" if pgm.process_group_manager.cp_world_size > 1 else "0"
     if zigzag is not None:
         os.environ["PICO_CP_ZIGZAG"] = "1" if zigzag else "0"
+    for m in model.modules():
+        refresh = getattr(m, "refresh_rope", None)
+        if callable(refresh):
+            refresh()
     return model
 
 
@@ -47,8 +55,8 @@ def zigzag_positions(seq_len, cp_rank, cp_world_size):
     assert seq_len % (2 * cp_world_size) == 0, \
         f"zig-zag context parallelism needs seq_len ({seq_len}) divisible by 2 * cp ({2 * cp_world_size})"
     c = seq_len // (2 * cp_world_size)
-    first = torch.arange(cp_rank * c, (cp_rank + 1) * c)
-    second = torch.arange((2 * cp_world_size - 1 - cp_rank) * c, (2 * cp_world_size - cp_rank) * c)
+    first = torch.arange(cp_rank * c, (cp_rank + 1) * c, device="cpu")
+    second = torch.arange((2 * cp_world_size - 1 - cp_rank) * c, (2 * cp_world_size - cp_rank) * c, device="cpu")
     return torch.cat([first, second])
 
 
@@ -63,9 +71,23 @@ def ring_attention(q, k, v, sm_scale, is_causal):
     return out.transpose(1, 2)
 
 
-def update_out_and_lse(out, lse, block_out, block_lse):
-    """Merge one block's (bf16 out [B,S,H,D], fp32 lse [B,H,S]) into the running fp32 (out, lse).
-    Returns the new (out, lse); the first call allocates them (ref :157-187)."""
+def _merge_launch(out, out_st, lse, lse_st, block_out, bo_st, block_lse, bl_st, B, S, H, D, first):
+    """pico_attn_merge on element strides: out / block_out (b, s, h) with unit d stride, lse / block_lse
+    (b, h, s)."""
+    ops._need(block_out, "block_out", None)
+    if block_out.dtype not in (torch.bfloat16, torch.float32):
+        raise TypeError(f"update_out_and_lse: block_out must be bf16 or fp32, got {block_out.dtype}")
+    for t, n in ((out, "out"), (lse, "lse"), (block_lse, "block_lse")):
+        ops._need(t, n, torch.float32)
+    _lib.check(_lib.load().pico_attn_merge(
+        _lib.ptr(out), _lib.i64x3(out_st), _lib.ptr(lse), _lib.i64x3(lse_st), _lib.ptr(block_out), _lib.i64x3(bo_st),
+        1 if block_out.dtype == torch.float32 else 0, _lib.ptr(block_lse), _lib.i64x3(bl_st), B, S, H, D,
+        1 if first else 0, _lib.stream_of(block_out)), "pico_attn_merge")
+
+
+def _merge_bshd(out, lse, block_out, block_lse):
+    """The ring's internal merge: block (out [B,S,H,D], lse [B,H,S]) into the running fp32 (out [B,S,H,D],
+    lse [B,H,S]); the first call allocates them. Same arithmetic as update_out_and_lse."""
     B, S, H, D = block_out.shape
     first = out is None
     if first:
@@ -73,10 +95,41 @@ def update_out_and_lse(out, lse, block_out, block_lse):
         lse = torch.empty((B, H, S), dtype=torch.float32, device=block_out.device)
     if block_out.stride(-1) != 1:
         block_out = block_out.contiguous()
-    lib = _lib.load()
-    _lib.check(lib.pico_attn_merge(_lib.ptr(out), _lib.ptr(lse), _lib.ptr(block_out), _lib.ptr(block_lse), B, S, H, D,
-                                   _lib.i64x3(block_out.stride()[:3]), 1 if first else 0,
-                                   _lib.stream_of(block_out)), "pico_attn_merge")
+    _merge_launch(out, out.stride()[:3], lse, lse.stride(), block_out, block_out.stride()[:3], block_lse,
+                  block_lse.stride(), B, S, H, D, first)
+    return out, lse
+
+
+def update_out_and_lse(out, lse, block_out, block_lse, slice_=None):
+    """ref :157-187, same signature and layout: block_out [B, H, S, D] (bf16 or fp32), block_lse [B, H, S];
+    the running out is fp32 [B, H, S, D] and lse fp32 [B, H, S, 1]. The first call (out None) returns
+    (block_out as fp32, block_lse[..., None]) as new tensors; later calls merge in place (the reference's
+    `_update` rebinds; its results are the same values) and return (out, lse). slice_ merges into
+    out[slice_] / lse[slice_] only (e.g. the rows of one query chunk), as the reference does; the first call
+    with a slice_ raises, as there. Runs on pico_attn_merge through element strides (no copies)."""
+    if block_out.dim() != 4 or block_lse.dim() != 3 or tuple(block_lse.shape) != tuple(block_out.shape[:3]):
+        raise ValueError("update_out_and_lse: block_out must be [B, H, S, D] and block_lse [B, H, S]")
+    if block_out.stride(-1) != 1:
+        block_out = block_out.contiguous()
+    B, H, S, D = block_out.shape
+    if out is None:
+        if slice_ is not None:
+            raise RuntimeError("first update_out_and_lse should not pass slice_ args")
+        out = torch.empty((B, H, S, D), dtype=torch.float32, device=block_out.device)
+        lse = torch.empty((B, H, S, 1), dtype=torch.float32, device=block_out.device)
+        first = True
+        ov, lv = out, lse
+    else:
+        first = False
+        ov, lv = (out[slice_], lse[slice_]) if slice_ is not None else (out, lse)
+    if ov.dim() != 4 or tuple(ov.shape) != (B, H, S, D) or ov.stride(-1) != 1 or \
+            lv.dim() != 4 or tuple(lv.shape) != (B, H, S, 1):
+        raise ValueError(f"update_out_and_lse: out{'[slice_]' if slice_ is not None else ''} must be [B, H, S, D] "
+                         f"with unit last stride and lse [B, H, S, 1] matching block_out {tuple(block_out.shape)}")
+    # [B, H, S, D] operands addressed as (b, s, h) rows; lse as (b, h, s)
+    ost, bst = ov.stride(), block_out.stride()
+    _merge_launch(ov, (ost[0], ost[2], ost[1]), lv, lv.stride()[:3], block_out, (bst[0], bst[2], bst[1]),
+                  block_lse, block_lse.stride(), B, S, H, D, first)
     return out, lse
 
 
@@ -104,7 +157,7 @@ class RingAttentionFunc(torch.autograd.Function):
                 comm.commit()
             if not is_causal or step <= comm.rank:
                 block_out, block_lse = ops.attention_block_fwd(q, k, v, sm_scale, is_causal and step == 0)
-                out, lse = update_out_and_lse(out, lse, block_out, block_lse)
+                out, lse = _merge_bshd(out, lse, block_out, block_lse)
             if step + 1 != comm.world_size:
                 comm.wait()
                 k, v = next_k, next_v
@@ -125,7 +178,7 @@ class RingAttentionFunc(torch.autograd.Function):
         halves = [[None, None], [None, None]]  # running fp32 (out, lse) of query chunks 0 and 1
 
         def merge(h, bo, bl):
-            halves[h][0], halves[h][1] = update_out_and_lse(halves[h][0], halves[h][1], bo, bl.contiguous())
+            halves[h][0], halves[h][1] = _merge_bshd(halves[h][0], halves[h][1], bo, bl)
 
         for step in range(n):
             if step + 1 != n:

@@ -234,8 +234,17 @@ class DecoderLayer(nn.Module):
         self.attention = Attention(config, layer_idx=layer_idx)
         self.mlp = MLP(config)
         self.layer_idx = layer_idx
-        head_dim = config.hidden_size // config.num_attention_heads
-        cos, sin = get_cos_sin(config.max_position_embeddings, head_dim=head_dim, base=config.rope_theta)
+        self._rope_geometry = (config.max_position_embeddings, config.hidden_size // config.num_attention_heads,
+                               config.rope_theta)
+        self.refresh_rope()
+
+    def refresh_rope(self):
+        """(Re)build this layer's cos/sin tables for the current context-parallel layout (ref
+        picotron/model.py:198-201): the cp rank's contiguous slice, or its two zig-zag chunks. Built at
+        construction like the reference; apply_context_parallel calls it again when it switches the layout
+        of an already built model (the reference's order: model first, then CP, ref train.py:175-188)."""
+        seq, head_dim, base = self._rope_geometry
+        cos, sin = get_cos_sin(seq, head_dim=head_dim, base=base)
         from .context_parallel.context_parallel import update_rope_for_context_parallel
         self.cos, self.sin = update_rope_for_context_parallel(cos, sin)
 

@@ -123,7 +123,7 @@ def test_ring_blocks_cp8_local_4096():
     (causal) and two earlier blocks (full) — merged in fp32 (3-block update_out_and_lse), then each block's
     backward fed the GLOBAL O / LSE with dQ accumulated in fp32, vs whole-sequence fp32 attention."""
     from picotron_amd import ops
-    from picotron_amd.context_parallel.context_parallel import update_out_and_lse
+    from picotron_amd.context_parallel.context_parallel import _merge_bshd
     torch.manual_seed(32768)
     B, n, H, D, nb = 1, 4096, 32, 64, 3
     sc = 1.0 / math.sqrt(D)
@@ -135,7 +135,7 @@ def test_ring_blocks_cp8_local_4096():
     for j in range(nb):  # ring order: own block (causal) first, then the earlier ones
         src = nb - 1 - j
         bo, bl = ops.attention_block_fwd(q, ks[src], vs[src], sc, src == nb - 1)
-        out, lse = update_out_and_lse(out, lse, bo, bl)
+        out, lse = _merge_bshd(out, lse, bo, bl)
     o = out.to(BF)
     kcat, vcat = torch.cat(ks, 1), torch.cat(vs, 1)
     O, L, (gq, gk, gv) = _attn_ref(q, kcat, vcat, do, sc, True, q_offset=(nb - 1) * n)

@@ -84,6 +84,43 @@ def test_loader_and_rope_follow_zigzag(monkeypatch):
     assert torch.equal(b["input_ids"], toks[:, r * S // n:(r + 1) * S // n])
 
 
+def test_apply_context_parallel_reslices_built_model_rope(monkeypatch):
+    """the reference builds the model first and applies CP afterwards (ref train.py:175-188).
+    apply_context_parallel(model, zigzag=True) on an already built model must re-slice every decoder layer's
+    RoPE tables to the zig-zag positions (and back to the contiguous slice with zigzag=False); checked against
+    the fp64 oracle's tables (oracle.hotpath.get_cos_sin, ref picotron/model.py:21-30) at those positions."""
+    from oracle import hotpath as H
+    from picotron_amd import process_group_manager as pgm
+    from picotron_amd.context_parallel import context_parallel as CP
+    from picotron_amd.model import Llama, LlamaConfig
+    S, n, r = 64, 4, 2
+    monkeypatch.setenv("DEVICE", "cpu")
+    monkeypatch.setenv("PICO_CP_ZIGZAG", "0")
+    monkeypatch.setattr(pgm, "process_group_manager",
+                        SimpleNamespace(tp_world_size=1, dp_world_size=1, dp_rank=0, cp_world_size=n, cp_rank=r))
+    cfg = LlamaConfig(hidden_size=128, intermediate_size=256, num_attention_heads=2, num_key_value_heads=2,
+                      num_hidden_layers=2, vocab_size=64, max_position_embeddings=S)
+    with torch.device("meta"):
+        model = Llama(cfg)
+    cos_ref, sin_ref = H.get_cos_sin(S, 64, cfg.rope_theta)
+    contiguous = torch.arange(r * S // n, (r + 1) * S // n)
+    zig = CP.zigzag_positions(S, r, n)
+    assert not torch.equal(contiguous, zig)
+
+    def check(pos):
+        for layer in model.decoder_layers:
+            assert layer.cos.shape == (S // n, 64)
+            assert torch.equal(layer.cos.double(), cos_ref[pos].double())
+            assert torch.equal(layer.sin.double(), sin_ref[pos].double())
+
+    check(contiguous)  # built under the contiguous layout
+    CP.apply_context_parallel(model, zigzag=True)
+    assert os.environ["PICO_CP_ZIGZAG"] == "1" and os.environ["CONTEXT_PARALLEL"] == "1"
+    check(zig)
+    CP.apply_context_parallel(model, zigzag=False)
+    check(contiguous)
+
+
 def _oracle_ops(CP, H):
     """attention_block_fwd/_bwd and update_out_and_lse on [B, S, H, D] tensors, computed by the oracle."""
     def fwd(q, k, v, scale, causal):
@@ -108,7 +145,7 @@ def _oracle_ops(CP, H):
 
     CP.ops.attention_block_fwd = fwd
     CP.ops.attention_block_bwd = bwd
-    CP.update_out_and_lse = merge
+    CP._merge_bshd = merge
 
 
 def _ring_worker(rank, world, port, zigzag, out_dir):

@@ -418,25 +418,54 @@ def test_attention_softmax_rescale_branch():
 
 # ------------------------------------------------------------------------------------------ ring merge
 def test_merge_golden(golden_kernels):
+    """update_out_and_lse with the reference's signature and layout (ref
+    picotron/context_parallel/context_parallel.py:157-187): block_out [B, H, S, D], block_lse [B, H, S]; the
+    running out fp32 [B, H, S, D] and lse [B, H, S, 1], against the reference-generated 3-block merge."""
     from picotron_amd.context_parallel.context_parallel import update_out_and_lse
     g = golden_kernels
     out = lse = None
     for i in range(3):
-        bo = g[f"merge.block_out{i}"].transpose(1, 2).contiguous().to(BF).to(DEV)  # [B,S,H,D]
-        out, lse = update_out_and_lse(out, lse, bo, g[f"merge.block_lse{i}"].to(DEV))
+        out, lse = update_out_and_lse(out, lse, g[f"merge.block_out{i}"].to(BF).to(DEV), g[f"merge.block_lse{i}"].to(DEV))
     ref_out, ref_lse = None, None
     for i in range(3):
         ref_out, ref_lse = H.update_out_and_lse(ref_out, ref_lse, g[f"merge.block_out{i}"].to(BF).double(),
                                                 g[f"merge.block_lse{i}"].double())
-    assert max_abs(out.transpose(1, 2).cpu(), ref_out) < 1e-5
-    assert max_abs(lse.cpu(), ref_lse.squeeze(-1)) < 1e-5
+    assert out.dtype == torch.float32 and out.shape == ref_out.shape and lse.shape == ref_lse.shape
+    assert max_abs(out.cpu(), ref_out) < 1e-5
+    assert max_abs(lse.cpu(), ref_lse) < 1e-5
+
+
+def test_merge_reference_slice_and_fp32_block():
+    """slice_ (ref :183-184: merge into out[slice_] / lse[slice_] only) on a query-row slice and a head slice,
+    fp32 block_out, and the first-call slice_ error, against the oracle's restatement of the same function."""
+    from picotron_amd.context_parallel.context_parallel import update_out_and_lse
+    torch.manual_seed(5)
+    B, Hh, S, D = 2, 4, 96, 64
+    blocks = [(torch.randn(B, Hh, S, D, device=DEV).to(BF), torch.randn(B, Hh, S, device=DEV) * 3) for _ in range(2)]
+    rows = (slice(None), slice(None), slice(32, None))
+    heads = (slice(None), slice(1, 3))
+    b2 = (torch.randn(B, Hh, S - 32, D, device=DEV), torch.randn(B, Hh, S - 32, device=DEV) * 3)  # fp32 block
+    b3 = (torch.randn(B, 2, S, D, device=DEV).to(BF), torch.randn(B, 2, S, device=DEV) * 3)
+    with pytest.raises(RuntimeError):
+        update_out_and_lse(None, None, *blocks[0], slice_=rows)
+    out = lse = None
+    ro = rl = None
+    for bo, bl in blocks:
+        out, lse = update_out_and_lse(out, lse, bo, bl)
+        ro, rl = H.update_out_and_lse(ro, rl, bo.cpu().double(), bl.cpu().double())
+    out, lse = update_out_and_lse(out, lse, *b2, slice_=rows)
+    ro, rl = H.update_out_and_lse(ro, rl, b2[0].cpu().double(), b2[1].cpu().double(), slice_=rows)
+    out, lse = update_out_and_lse(out, lse, *b3, slice_=heads)
+    ro, rl = H.update_out_and_lse(ro, rl, b3[0].cpu().double(), b3[1].cpu().double(), slice_=heads)
+    assert max_abs(out.cpu(), ro) < 1e-5
+    assert max_abs(lse.cpu(), rl) < 1e-5
 
 
 def test_ring_attention_single_process_blocks():
     """Causal attention over a sequence split in 4 blocks, merged with the kernels the way the ring
     does (step s computes q_r against kv_{r-s}), equals whole-sequence attention."""
     ops = _ops()
-    from picotron_amd.context_parallel.context_parallel import update_out_and_lse
+    from picotron_amd.context_parallel.context_parallel import _merge_bshd
     torch.manual_seed(11)
     B, S, Hh, D, W = 1, 512, 2, 64, 4
     q, k, v = [torch.randn(B, S, Hh, D, dtype=BF, device=DEV) for _ in range(3)]
@@ -448,7 +477,7 @@ def test_ring_attention_single_process_blocks():
             src = r - step
             bo, bl = ops.attention_block_fwd(q[:, r * n:(r + 1) * n], k[:, src * n:(src + 1) * n],
                                              v[:, src * n:(src + 1) * n], 0.125, step == 0)
-            out, lse = update_out_and_lse(out, lse, bo, bl)
+            out, lse = _merge_bshd(out, lse, bo, bl)
         assert rel_l2(out.cpu(), full[:, r * n:(r + 1) * n].float().cpu()) < 4e-3
 
 
