@@ -221,6 +221,8 @@ def main():
     dist.barrier()
     elapsed = time.perf_counter() - t_start
     losses = [float(l) for l in losses]
+    from picotron_amd import ops as _ops
+    _ops.check_lm_head_grad_scale()  # the chunked CE's unit-upstream contract held over the timed steps
     t = torch.tensor([elapsed], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())

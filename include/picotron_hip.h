@@ -263,16 +263,20 @@ int pico_cross_entropy_fwd_grad(void* logits, int64_t ld, const int64_t* target,
 /* The mean's scalars around pico_cross_entropy_fwd_grad, one launch each (instead of the ATen scalar ops of
  * F.cross_entropy(reduction='mean')'s host code): pico_ce_count writes stats[0] = #(target != ignore_index),
  * stats[1] = grad_scale / stats[0] (pass stats + 1 as fwd_grad's grad_scale); pico_ce_mean writes
- * grad_scale * sum(loss_rows) / stats[0] to *out (bf16, or fp32 when out_f32), summed in a fixed order. */
+ * grad_scale * sum(loss_rows) / stats[0] to *out (bf16, or fp32 when out_f32), summed in a fixed order,
+ * and when acc is non-null adds the stored value to *acc (fp32): the training loop's per-step loss sum
+ * (ref train.py:53 `loss_acc += loss.item()`), kept on the device without a separate launch. */
 int pico_ce_count(const int64_t* target, int64_t n, int64_t ignore_index, float grad_scale, float* stats,
                   void* stream);
 int pico_ce_mean(const float* loss_rows, int64_t n, const float* stats, float grad_scale, void* out, int out_f32,
-                 void* stream);
+                 float* acc, void* stream);
 /* backward of the fused LM-head CE: dx (bf16, contiguous, n elements) *= *upstream (the loss's upstream
  * gradient, a device 0-dim bf16 tensor, or fp32 when upstream_f32, rounded to bf16 first as ATen does),
  * fp32 product, one bf16 rounding.
- * Replaces autograd's scaling of the reference's logits gradient (ref picotron/model.py:269, train.py:46-49). */
-int pico_ce_scale_grad(void* dx, int64_t n, const void* upstream, int upstream_f32, void* stream);
+ * Replaces autograd's scaling of the reference's logits gradient (ref picotron/model.py:269, train.py:46-49).
+ * nonunit (optional, device int): set to 1 if the upstream gradient is not exactly 1 (the chunked LM-head CE
+ * accumulated its weight gradient in the forward for a unit upstream; the host checks the flag later). */
+int pico_ce_scale_grad(void* dx, int64_t n, const void* upstream, int upstream_f32, int* nonunit, void* stream);
 int pico_cross_entropy_bwd(const void* logits, int64_t ld, const int64_t* target, const float* lse,
                            const float* grad_scale, void* dlogits, int64_t ldd, int64_t rows, int64_t vocab,
                            int64_t ignore_index, void* stream);

@@ -91,8 +91,8 @@ _SIGNATURES = {
     "pico_cross_entropy_fwd": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp]),
     "pico_cross_entropy_fwd_grad": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp]),
     "pico_ce_count": (ctypes.c_int, [c_vp, c_i64, c_i64, ctypes.c_float, c_vp, c_vp]),
-    "pico_ce_mean": (ctypes.c_int, [c_vp, c_i64, c_vp, ctypes.c_float, c_vp, ctypes.c_int, c_vp]),
-    "pico_ce_scale_grad": (ctypes.c_int, [c_vp, c_i64, c_vp, ctypes.c_int, c_vp]),
+    "pico_ce_mean": (ctypes.c_int, [c_vp, c_i64, c_vp, ctypes.c_float, c_vp, ctypes.c_int, c_vp, c_vp]),
+    "pico_ce_scale_grad": (ctypes.c_int, [c_vp, c_i64, c_vp, ctypes.c_int, c_vp, c_vp]),
     "pico_cross_entropy_bwd": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp]),
     "pico_transpose_bf16": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_i64, c_i64, c_vp]),
 }

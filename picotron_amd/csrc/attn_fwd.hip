@@ -390,8 +390,10 @@ __attribute__((amdgpu_waves_per_eu(FwdCfg<D>::WAVES_PER_EU, FwdCfg<D>::WAVES_PER
       for (int j = 0; j < 8; ++j) {
         const float xa = bf2f(x1[j]), xb = bf2f(x2[j]);
         const float cf = bf2f(rc[ks][j]), sf = bf2f(rs[ks][j]);
-        o1[j] = f2bf(xa * cf - xb * sf);
-        o2[j] = f2bf(xb * cf + xa * sf);
+        // both products rounded before the sum (no FMA contraction): the rope kernel's and the oracle's
+        // fp32 arithmetic bit for bit, so q rotated here == pico_rope's q
+        o1[j] = f2bf(__fmul_rn(xa, cf) - __fmul_rn(xb, sf));
+        o2[j] = f2bf(__fmul_rn(xb, cf) + __fmul_rn(xa, sf));
       }
       qf[ks] = __builtin_bit_cast(bf16x8, o1);
       qf[ks + KS / 2] = __builtin_bit_cast(bf16x8, o2);

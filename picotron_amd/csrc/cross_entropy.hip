@@ -256,7 +256,8 @@ extern "C" int pico_cross_entropy_bwd(const void* logits, int64_t ld, const int6
 //   pico_ce_count: stats[0] = number of targets != ignore_index, stats[1] = grad_scale / stats[0]
 //     (the per-row gradient scale pico_cross_entropy_fwd_grad reads);
 //   pico_ce_mean: out (bf16, or fp32 when out_f32) = grad_scale * sum(loss_rows) / stats[0],
-//     summed in a fixed order (deterministic).
+//     summed in a fixed order (deterministic); acc (optional, fp32) += that value as stored in out — the
+//     training loop's per-step loss sum (`loss_acc += loss`, ref train.py:53) without a separate launch.
 namespace {
 constexpr int CE_NT = 1024;
 
@@ -285,15 +286,21 @@ __global__ __launch_bounds__(CE_NT) void ce_count_kernel(const int64_t* __restri
 
 __global__ __launch_bounds__(CE_NT) void ce_mean_kernel(const float* __restrict__ loss_rows, int64_t n,
                                                         const float* __restrict__ stats, float grad_scale, void* out,
-                                                        int out_f32) {
+                                                        int out_f32, float* acc) {
   __shared__ float red[CE_NT / 64];
   float s = 0.f;
   for (int64_t i = threadIdx.x; i < n; i += CE_NT) s += loss_rows[i];
   const float t = block_sum_1024(s, red);
   if (threadIdx.x == 0) {
-    const float v = t / stats[0] * grad_scale;
-    if (out_f32) *(float*)out = v;
-    else *(bf16_t*)out = f2bf(v);
+    float v = t / stats[0] * grad_scale;
+    if (out_f32) {
+      *(float*)out = v;
+    } else {
+      const bf16_t b = f2bf(v);
+      *(bf16_t*)out = b;
+      v = bf2f(b);
+    }
+    if (acc) *acc += v;
   }
 }
 }  // namespace
@@ -306,9 +313,9 @@ extern "C" int pico_ce_count(const int64_t* target, int64_t n, int64_t ignore_in
 }
 
 extern "C" int pico_ce_mean(const float* loss_rows, int64_t n, const float* stats, float grad_scale, void* out,
-                            int out_f32, void* stream) {
+                            int out_f32, float* acc, void* stream) {
   PICO_REQUIRE(loss_rows && stats && out && n >= 0, "pico_ce_mean: bad arguments");
-  PICO_TRY(pico_launch(PICO_K_CE_FWD, "ce_mean", ce_mean_kernel, dim3(1), dim3(CE_NT), 0, (hipStream_t)stream, loss_rows, n, stats, grad_scale, out, out_f32));
+  PICO_TRY(pico_launch(PICO_K_CE_FWD, "ce_mean", ce_mean_kernel, dim3(1), dim3(CE_NT), 0, (hipStream_t)stream, loss_rows, n, stats, grad_scale, out, out_f32, acc));
   return 0;
 }
 
@@ -318,11 +325,15 @@ extern "C" int pico_ce_mean(const float* loss_rows, int64_t n, const float* stat
 // rounding as ATen's bf16 tensor * 0-dim tensor (the 0-dim operand cast to bf16 first, then an fp32
 // product and one bf16 rounding), without the
 // broadcasting elementwise kernel that op lowers to (≈ 33 us per micro-batch at 4096 x 2048; this one
-// streams 16-byte vectors).
+// streams 16-byte vectors). nonunit (optional): set to 1 when the upstream gradient is not exactly 1 — the
+// chunked LM-head CE took its weight gradient in the forward for a unit upstream, and the host reports a
+// violation the next time it reads this flag (no synchronisation here).
 namespace {
 __global__ __launch_bounds__(256) void scale_by_dev_kernel(bf16_t* __restrict__ x, int64_t n,
-                                                           const void* __restrict__ g, int g_f32) {
-  const float s = bf2f(g_f32 ? f2bf(*(const float*)g) : *(const bf16_t*)g);
+                                                           const void* __restrict__ g, int g_f32, int* nonunit) {
+  const float graw = g_f32 ? *(const float*)g : bf2f(*(const bf16_t*)g);
+  const float s = bf2f(g_f32 ? f2bf(graw) : *(const bf16_t*)g);
+  if (nonunit && blockIdx.x == 0 && threadIdx.x == 0 && graw != 1.f) *nonunit = 1;
   const int64_t nv = n / 8;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nv; i += (int64_t)gridDim.x * 256) {
     u16x8 v = reinterpret_cast<u16x8*>(x)[i];
@@ -334,13 +345,14 @@ __global__ __launch_bounds__(256) void scale_by_dev_kernel(bf16_t* __restrict__ 
 }
 }  // namespace
 
-extern "C" int pico_ce_scale_grad(void* dx, int64_t n, const void* upstream, int upstream_f32, void* stream) {
+extern "C" int pico_ce_scale_grad(void* dx, int64_t n, const void* upstream, int upstream_f32, int* nonunit,
+                                  void* stream) {
   PICO_REQUIRE(dx && upstream && n >= 0, "pico_ce_scale_grad: bad arguments");
   PICO_REQUIRE((uintptr_t)dx % 16 == 0, "pico_ce_scale_grad: dx must be 16-byte aligned");
   if (n == 0) return 0;
   int64_t nb = (n / 8 + 255) / 256;
   if (nb < 1) nb = 1;
   if (nb > 4096) nb = 4096;
-  PICO_TRY(pico_launch(PICO_K_CE_BWD, "ce_scale_grad", scale_by_dev_kernel, dim3((int)nb), dim3(256), 0, (hipStream_t)stream, (bf16_t*)dx, n, upstream, upstream_f32));
+  PICO_TRY(pico_launch(PICO_K_CE_BWD, "ce_scale_grad", scale_by_dev_kernel, dim3((int)nb), dim3(256), 0, (hipStream_t)stream, (bf16_t*)dx, n, upstream, upstream_f32, nonunit));
   return 0;
 }

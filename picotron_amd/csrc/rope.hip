@@ -37,8 +37,10 @@ __global__ __launch_bounds__(256) void rope_kernel(const bf16_t* __restrict__ x,
     for (int j = 0; j < 8; ++j) {
       const float a = bf2f(x1[j]), bb = bf2f(x2[j]);
       const float cf = bf2f(c[j]), sf = sign * bf2f(sn[j]);
-      o1[j] = f2bf(a * cf - bb * sf);
-      o2[j] = f2bf(bb * cf + a * sf);
+      // products rounded before the sum (no FMA contraction: flash-attn's fp32 rotary / the oracle's
+      // restatement, and the same arithmetic as the q rotation inside the attention forward)
+      o1[j] = f2bf(__fmul_rn(a, cf) - __fmul_rn(bb, sf));
+      o2[j] = f2bf(__fmul_rn(bb, cf) + __fmul_rn(a, sf));
     }
     *reinterpret_cast<u16x8*>(op) = o1;
     *reinterpret_cast<u16x8*>(op + half) = o2;

@@ -70,6 +70,10 @@ class DataParallelBucket(nn.Module):
         self._post_backward_callback_set = False
 
     def forward(self, *inputs, **kwargs):
+        # no backward pass is in flight while the host runs a forward: per-pass state left by a backward that
+        # raised midway (its end-of-pass callbacks never ran) is dropped here
+        self._end_pass()
+        self._post_backward_callback_set = False
         return self.module(*inputs, **kwargs)
 
     def backward(self, input_tensor, output_tensor, output_tensor_grad):
@@ -149,3 +153,5 @@ class DataParallelBucket(nn.Module):
 
     def reset(self):
         self.bucket_manager.reset()
+        self._end_pass()
+        self._post_backward_callback_set = False

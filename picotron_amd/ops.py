@@ -45,6 +45,10 @@ class _RMSNormFn(torch.autograd.Function):
     def forward(ctx, x, residual, weight, eps, prenorm, want_t=False):
         _need(x, "x")
         _need(weight, "weight")
+        # a chained dw left pending means the backward pass that created it raised before its end-of-pass
+        # flush ran (no backward pass is in flight during a forward): drop it
+        if _NORM_PENDING:
+            _NORM_PENDING.pop(x.device, None)
         shape = x.shape
         cols = shape[-1]
         x2 = x.reshape(-1, cols).contiguous()
@@ -368,16 +372,22 @@ def wgrad_accumulate(params, dy2, x2):
 # dx = dy W runs on hipBLASLt ~7-20 % slower in that (NN) form than the same product in the forward's
 # form F.linear(dy, W^T) against a contiguous W^T (measured on MI355X at M = 4096: gate_up 243 -> 213 us,
 # down 117 -> 97, qkv 104 -> 97, lm_head 634 -> 588; scripts/gemm_layout_probe.py). W^T is kept per
-# weight (bf16, +1 copy of the weights in HBM) and re-transposed only when the weights changed: after
-# any optimizer step (a global step post-hook bumps a generation; the fused AdamW does not bump the
-# parameters' version counters) or an in-place write that bumps a version counter.
-# refresh_weight_transposes() brings every cached copy up to date eagerly; MicroBatchGraph calls it
-# before each replay (a replayed graph runs no host code, so it could not notice stale copies).
-# Writes that bump neither counter — through `p.data` (p.data.copy_(), a checkpoint load into .data),
-# or by an optimizer that is not a torch.optim.Optimizer — must be followed by
-# invalidate_weight_transposes(). Entries are keyed by the weight's storage (identity and data pointer)
-# and shape, and hold the parameters W is made of only through weak references: a rebuilt model does
-# not keep the old one's weights alive, and entries whose parameters died are dropped.
+# weight (bf16, +1 copy of the weights in HBM) and re-transposed lazily, at its next use, whenever the
+# weights may have changed. Safe by default — every way a drop-in caller writes weights
+# is seen:
+#   * an optimizer step (a global torch.optim step post-hook bumps a generation; the fused AdamW does not
+#     bump the parameters' version counters);
+#   * an in-place write through the parameter itself (`with no_grad(): p.copy_(x)`, load_state_dict): its
+#     version counter;
+#   * any access to a parameter's `.data` (p.data.copy_(x), p.data.mul_(2), p.data = t, module.to()): the
+#     `.data` property of torch.nn.Parameter is wrapped on first use of the cache to bump the generation
+#     (a write through `.data` bumps no version counter, and torch exposes no other hook for it). Every
+#     access counts as a possible write; the product path itself touches `.data` only at setup.
+#   * a parameter re-pointed at other storage: entries are keyed by the weight's storage and data pointer.
+# Not seen: a tensor obtained from `.data` earlier and written after the next use, and raw writes to
+# p.data_ptr() by foreign kernels; invalidate_weight_transposes() covers those. MicroBatchGraph calls
+# refresh_weight_transposes() before each replay (a replayed graph runs no host code). Entries hold their
+# parameters only through weak references: a rebuilt model does not keep the old one's weights alive.
 # --------------------------------------------------------------------------------------------
 _WT_GEN = [0]
 _WT_CACHE = {}  # (storage id, W.data_ptr(), shape) -> [wt, key, [weakref(p) for p in params]]
@@ -388,9 +398,27 @@ def _bump_wt_gen(*_):
     _WT_GEN[0] += 1
 
 
+def _watch_parameter_data():
+    """Wrap torch.nn.Parameter.data (getter and setter) so that any `.data` access bumps the W^T generation."""
+    if getattr(torch.nn.Parameter, "_pico_data_watched", False):
+        return
+    desc = torch._C.TensorBase.__dict__["data"]
+
+    def _get(self):
+        _WT_GEN[0] += 1
+        return desc.__get__(self)
+
+    def _set(self, value):
+        _WT_GEN[0] += 1
+        desc.__set__(self, value)
+
+    torch.nn.Parameter.data = property(_get, _set, doc=desc.__doc__)
+    torch.nn.Parameter._pico_data_watched = True
+
+
 def invalidate_weight_transposes():
-    """Mark every cached W^T stale (re-transposed on next use): call after writing weights through
-    `.data` or with a non-torch.optim optimizer."""
+    """Mark every cached W^T stale (re-transposed on next use). Not needed after optimizer steps, in-place
+    writes or `.data` writes (all detected); only after raw writes to a parameter's storage by foreign code."""
     _bump_wt_gen()
 
 
@@ -412,6 +440,7 @@ def weight_t(W, params):
     """Contiguous W^T ([K, N] for W [N, K]), up to date with the parameters `params` W is made of."""
     if not _WT_HOOK:
         _WT_HOOK.append(_register_step_post_hook(_bump_wt_gen))
+        _watch_parameter_data()
     key = (_WT_GEN[0],) + tuple(p._version for p in params)
     ck = _wt_key(W)
     ent = _WT_CACHE.get(ck)
@@ -654,16 +683,47 @@ class _LMHeadCEFn(torch.autograd.Function):
         return dx, dw, None, None
 
 
-def _scale_by_upstream(dx, grad_out):
+def _scale_by_upstream(dx, grad_out, nonunit=None):
     """dx (bf16, contiguous) *= the loss's upstream gradient, read on the device (pico_ce_scale_grad: same
-    rounding as ATen's dx.mul_(grad_out), one streaming launch instead of a cast + a broadcasting ATen mul)."""
+    rounding as ATen's dx.mul_(grad_out), one streaming launch instead of a cast + a broadcasting ATen mul).
+    nonunit (int32 device tensor): set to 1 by the same launch when the upstream gradient is not exactly 1."""
     if dx.dtype != torch.bfloat16 or not dx.is_contiguous() or grad_out.dtype not in (torch.bfloat16, torch.float32):
+        if nonunit is not None:
+            nonunit.copy_(torch.maximum(nonunit, (grad_out != 1).to(nonunit.dtype)))
         return dx.mul_(grad_out.to(torch.float32))
     g = grad_out if grad_out.is_contiguous() else grad_out.contiguous()
     _lib.check(_lib.load().pico_ce_scale_grad(_lib.ptr(dx), dx.numel(), _lib.ptr(g),
-                                              1 if g.dtype == torch.float32 else 0, _lib.stream_of(dx)),
-               "pico_ce_scale_grad")
+                                              1 if g.dtype == torch.float32 else 0, _lib.ptr(nonunit),
+                                              _lib.stream_of(dx)), "pico_ce_scale_grad")
     return dx
+
+
+# device -> int32 flag set when a chunked LM-head CE (grad_scale=...) was back-propagated with an upstream
+# gradient other than 1 (its weight gradient, taken in the forward, assumed 1): read by check_lm_head_grad_scale
+_CE_NONUNIT = {}
+
+
+def _ce_nonunit_flag(dev):
+    f = _CE_NONUNIT.get(dev)
+    if f is None:
+        f = _CE_NONUNIT[dev] = torch.zeros((), dtype=torch.int32, device=dev)
+    return f
+
+
+def check_lm_head_grad_scale(device=None):
+    """Raise if any chunked lm_head_cross_entropy(grad_scale=...) since the last check received an upstream
+    gradient other than exactly 1 — its dx was scaled correctly, but the weight gradient it accumulated in the
+    forward was not. Reads one device int (a host sync): train_step calls it where it reads the
+    loss anyway. Resets the flag."""
+    for dev, f in list(_CE_NONUNIT.items()):
+        if device is not None and torch.device(device) != torch.device(dev):
+            continue
+        if int(f.item()) != 0:
+            f.zero_()
+            raise RuntimeError("lm_head_cross_entropy(grad_scale=s) was back-propagated with an upstream gradient "
+                               "other than 1: its weight gradient (taken in the forward for a unit upstream) is "
+                               "wrong. Fold every loss scale into grad_scale and call loss.backward() on the "
+                               "returned loss alone, or use the unchunked form (grad_scale=None).")
 
 
 class _LMHeadCEChunkedFn(torch.autograd.Function):
@@ -676,12 +736,18 @@ class _LMHeadCEChunkedFn(torch.autograd.Function):
     micro-batch, the bf16 .grad, or a buffer handed to autograd). The backward only scales the saved dx
     by the upstream gradient and marks the weight ready for the DP bucket.
 
-    Contract: grad_scale is the gradient the loss will receive (the training loop's 1 / grad_acc folded
-    in here instead of dividing the loss; loss.backward() then feeds 1). dx stays exact for any upstream
-    gradient; the already-accumulated dW assumes it is 1 (PICO_CHECK_GRAD_SCALE=1 asserts it, with a sync)."""
+    CONTRACT — the returned loss MUST be back-propagated with an upstream gradient of exactly 1: grad_scale is
+    the gradient the loss will receive (the training loop's 1 / grad_acc folded in here instead of dividing
+    the loss; loss.backward() then feeds 1). dx stays exact for any upstream gradient, but dW is accumulated
+    in the forward for a unit upstream. A violation (a loss scaler, a weighted sum with another loss,
+    autograd.grad with other grad_outputs) is recorded on the device by the backward's own launch and raised
+    by check_lm_head_grad_scale(), which train_step runs whenever it reads the loss (PICO_CHECK_GRAD_SCALE=1
+    checks inside the backward instead, with a host sync).
+    loss_acc (optional fp32 0-dim device tensor): += the returned loss, inside the pico_ce_mean launch (the
+    micro-batch graph's loss sum, no separate add node)."""
 
     @staticmethod
-    def forward(ctx, x, w, target, ignore_index, grad_scale, chunk):
+    def forward(ctx, x, w, target, ignore_index, grad_scale, chunk, loss_acc=None):
         _need(x, "x")
         _need(w, "w")
         H = x.shape[-1]
@@ -759,8 +825,11 @@ class _LMHeadCEChunkedFn(torch.autograd.Function):
             if side is not None:
                 torch.cuda.current_stream(x.device).wait_stream(side)
         loss = torch.empty((), dtype=x.dtype, device=x.device)
+        if loss_acc is not None:
+            _need(loss_acc, "loss_acc", torch.float32)
         _lib.check(lib.pico_ce_mean(_lib.ptr(loss_rows), T, _lib.ptr(stats), float(grad_scale), _lib.ptr(loss),
-                                    1 if x.dtype == torch.float32 else 0, _lib.stream_of(x)), "pico_ce_mean")
+                                    1 if x.dtype == torch.float32 else 0, _lib.ptr(loss_acc), _lib.stream_of(x)),
+                   "pico_ce_mean")
         ctx.save_for_backward(dx)
         ctx.xshape = x.shape
         ctx.dw = dst if kind == "autograd_acc" else None
@@ -773,13 +842,16 @@ class _LMHeadCEChunkedFn(torch.autograd.Function):
         if os.getenv("PICO_CHECK_GRAD_SCALE", "0") == "1":
             assert float(grad_out) == 1.0, f"lm_head_cross_entropy(grad_scale=...): upstream gradient {float(grad_out)} != 1"
         dxo = None
+        flag = _ce_nonunit_flag(dx.device)
         if ctx.needs_input_grad[0]:
-            dxo = _scale_by_upstream(dx, grad_out).view(ctx.xshape)
+            dxo = _scale_by_upstream(dx, grad_out, flag).view(ctx.xshape)
+        else:
+            flag.copy_(torch.maximum(flag, (grad_out != 1).to(flag.dtype)))
         if ctx.ready is not None:
             ctx.ready()
         dw = ctx.dw
         ctx.dw = None
-        return dxo, dw, None, None, None, None
+        return dxo, dw, None, None, None, None, None
 
 
 def ce_chunk_rows():
@@ -787,15 +859,19 @@ def ce_chunk_rows():
     return int(os.getenv("PICO_CE_CHUNK", "4096"))
 
 
-def lm_head_cross_entropy(x, w, target, ignore_index=-100, grad_scale=None, chunk=None):
+def lm_head_cross_entropy(x, w, target, ignore_index=-100, grad_scale=None, chunk=None, loss_acc=None):
     """mean cross-entropy of the LM head x W^T against target, fused. grad_scale=None: the drop-in form
-    (_LMHeadCEFn, logits [T, V] kept for the backward GEMMs). grad_scale=s: returns s * mean CE, computed
-    chunk rows at a time with dx and dW in the forward (_LMHeadCEChunkedFn; the loss must then be
-    back-propagated with unit gradient)."""
+    (_LMHeadCEFn, logits [T, V] kept for the backward GEMMs; exact for any upstream gradient).
+    grad_scale=s: returns s * mean CE, computed chunk rows at a time with dx and dW in the forward
+    (_LMHeadCEChunkedFn). !! The returned loss MUST then be back-propagated with an upstream gradient of
+    exactly 1 (plain loss.backward() on it alone) — the weight gradient is taken in the forward; a violation
+    raises at the next check_lm_head_grad_scale() (train_step runs it). loss_acc: see _LMHeadCEChunkedFn."""
     if grad_scale is None:
+        if loss_acc is not None:
+            raise ValueError("lm_head_cross_entropy: loss_acc needs the chunked form (grad_scale=...)")
         return _LMHeadCEFn.apply(x, w, target, ignore_index)
     return _LMHeadCEChunkedFn.apply(x, w, target, ignore_index, float(grad_scale),
-                                    ce_chunk_rows() if chunk is None else int(chunk))
+                                    ce_chunk_rows() if chunk is None else int(chunk), loss_acc)
 
 
 def cross_entropy(logits, target, ignore_index=-100, reduction="mean"):

@@ -29,7 +29,9 @@ class AdamW(torch.optim.Optimizer):
         self._tables = {}
 
     def _group_tables(self, gi, params):
-        key = (gi, tuple(p.data_ptr() for p in params))
+        # keyed by pointer AND size: a parameter re-pointed at a different-sized tensor that the caching
+        # allocator placed at the same address gets new size / chunk tables
+        key = (gi, tuple((p.data_ptr(), p.numel()) for p in params))
         ent = self._tables.get(key)
         if ent is None:
             chunk = int(_lib.load().pico_adamw_chunk_elems())

@@ -38,13 +38,18 @@ def _fused_lm_head(model):
     return head
 
 
-def _micro_batch(model, input_ids, target_ids, grad_acc_steps):
+def _micro_batch(model, input_ids, target_ids, grad_acc_steps, loss_acc=None):
+    """One micro-batch forward + backward (ref train.py:39-51); returns the detached loss. loss_acc (fp32 device
+    scalar): += the loss — inside the fused CE's mean launch when the chunked form runs, else one add."""
     head = _fused_lm_head(model)
+    folded = False
     if head is not None:  # fused LM head + cross-entropy (SURVEY §8f row 1): logits never re-read
         from . import ops
         h = model(input_ids=input_ids, return_hidden=True)
         if ops.ce_chunk_rows() > 0:  # chunked: 1 / grad_acc folded into the op (its dW is taken in the forward)
-            loss = ops.lm_head_cross_entropy(h, head.weight, target_ids.reshape(-1), grad_scale=1.0 / grad_acc_steps)
+            loss = ops.lm_head_cross_entropy(h, head.weight, target_ids.reshape(-1), grad_scale=1.0 / grad_acc_steps,
+                                             loss_acc=loss_acc)
+            folded = loss_acc is not None
         else:
             loss = ops.lm_head_cross_entropy(h, head.weight, target_ids.reshape(-1)) / grad_acc_steps
     else:
@@ -53,6 +58,8 @@ def _micro_batch(model, input_ids, target_ids, grad_acc_steps):
         outputs = outputs.view(seq_len * batch_size, -1)
         loss = _cross_entropy(outputs, target_ids.reshape(-1)) / grad_acc_steps
     loss.backward()
+    if loss_acc is not None and not folded:
+        loss_acc += loss.detach()
     return loss.detach()
 
 
@@ -83,7 +90,12 @@ def train_step(model, data_loader, device, graphs=None, sync_loss=True):
         losses.append(graphs.take_loss())
     # one host sync per step instead of one per micro-batch (ref :53 calls .item() each time), or none
     total = torch.stack(losses).float().sum() if losses else torch.zeros((), device=device)
-    return float(total.item()) if sync_loss else total
+    if not sync_loss:
+        return total
+    value = float(total.item())
+    from . import ops
+    ops.check_lm_head_grad_scale()  # the host just synchronised: a free read of the chunked CE's contract flag
+    return value
 
 
 class MicroBatchGraph:
@@ -106,7 +118,7 @@ class MicroBatchGraph:
         self.loss_acc = None
 
     def _fwd_bwd(self):
-        self.loss_acc += _micro_batch(self.model, self.inp, self.tgt, self.n)
+        _micro_batch(self.model, self.inp, self.tgt, self.n, loss_acc=self.loss_acc)
 
     def _capture(self, input_ids, target_ids):
         self.inp = input_ids.clone()

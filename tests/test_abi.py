@@ -112,25 +112,46 @@ def test_ops_fail_loudly_without_hip_tensors(lib):
 
 
 def test_weight_transpose_cache_host_logic(monkeypatch):
-    """ops.weight_t's cache: one entry per weight storage, reused across the fresh stacked
-    views each call builds; invalidate_weight_transposes() after a .data write (no version bump) makes the
-    next use re-transpose; entries hold their parameters only weakly and die with them. (CPU tensors: the
-    transpose falls back to a strided copy; the cache logic is the same.)"""
+    """ops.weight_t's cache: one entry per weight storage, reused across the fresh stacked views each call
+    builds; safe by default — writes through `.data` (no version bump), in-place writes
+    through the parameter (version bump), `.data` rebinds and optimizer steps all make the next use
+    re-transpose, with no explicit invalidate_weight_transposes(); entries hold their parameters only weakly
+    and die with them. (CPU tensors: the transpose falls back to a strided copy; the cache logic is the same.)"""
     import gc
     from picotron_amd import ops
     monkeypatch.setattr(ops, "_WT_CACHE", {})
-    monkeypatch.setattr(ops, "_WT_HOOK", [None])
+    monkeypatch.setattr(ops, "_WT_HOOK", [])
     a = torch.nn.Parameter(torch.randn(8, 16))
     b = torch.nn.Parameter(torch.randn(8, 16))
+
+    def fresh():
+        return torch.equal(ops.weight_t(ops.stacked_weight((a, b)), (a, b)), torch.cat([a, b]).t())
+
     t1 = ops.weight_t(ops.stacked_weight((a, b)), (a, b))
     assert torch.equal(t1, torch.cat([a, b]).t())
     assert ops.weight_t(ops.stacked_weight((a, b)), (a, b)) is t1 and len(ops._WT_CACHE) == 1
+    gen = ops._WT_GEN[0]
+    assert ops.weight_t(ops.stacked_weight((a, b)), (a, b)) is t1 and ops._WT_GEN[0] == gen  # no spurious bumps
     with torch.no_grad():
-        a.data.mul_(2)  # bumps no version counter the cache sees
-    assert not torch.equal(ops.weight_t(ops.stacked_weight((a, b)), (a, b)), torch.cat([a, b]).t())
-    ops.invalidate_weight_transposes()
-    assert torch.equal(ops.weight_t(ops.stacked_weight((a, b)), (a, b)), torch.cat([a, b]).t())
-    del a, b, t1
+        a.data.mul_(2)  # bumps no version counter: seen through the watched .data property
+    assert fresh()
+    b.data.copy_(torch.randn(8, 16))
+    assert fresh()
+    with torch.no_grad():
+        a.add_(1.0)  # version counter
+    assert fresh()
+    opt = torch.optim.SGD([a, b], lr=0.5)
+    a.grad, b.grad = torch.ones_like(a), torch.ones_like(b)
+    opt.step()  # step post-hook
+    assert fresh()
+    m = torch.nn.Linear(16, 8, bias=False)
+    tm = ops.weight_t(m.weight.detach(), (m.weight,))
+    m.load_state_dict({"weight": torch.randn(8, 16)})
+    assert torch.equal(ops.weight_t(m.weight.detach(), (m.weight,)), m.weight.t())
+    assert tm is ops.weight_t(m.weight.detach(), (m.weight,))  # same entry, refreshed in place
+    ops.invalidate_weight_transposes()  # still available for raw writes by foreign code
+    assert fresh()
+    del a, b, t1, m, tm, opt
     gc.collect()
     ops._wt_purge()
     assert len(ops._WT_CACHE) == 0
