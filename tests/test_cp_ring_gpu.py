@@ -53,7 +53,7 @@ def _staged_comm_class(base):
     return HostStagedCommunicate
 
 
-def _worker(rank, world, port, causal, zigzag=False):
+def _worker(rank, world, port, causal, zigzag=False, S=1024):
     import sys
     sys.path.insert(0, ROOT)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -68,7 +68,7 @@ def _worker(rank, world, port, causal, zigzag=False):
     CP.ContextCommunicate = _staged_comm_class(CP.ContextCommunicate)
 
     dev = "cuda:0"
-    B, S, Hq, D = 2, 1024, 4, 64
+    B, Hq, D = 2, 4, 64
     g = torch.Generator(device="cpu").manual_seed(21)  # identical full tensors on every rank
     q, k, v, do = [torch.randn(B, S, Hq, D, generator=g).to(BF).to(dev) for _ in range(4)]
     scale = D ** -0.5
@@ -102,11 +102,14 @@ def _worker(rank, world, port, causal, zigzag=False):
         raise AssertionError(f"rank {rank} cp={world} causal={causal} zigzag={zigzag}: {bad} (all: {errs})")
 
 
-@pytest.mark.parametrize("world,causal,zigzag", [(2, True, False), (4, True, False), (2, False, False),
-                                                 (2, True, True), (4, True, True)])
-def test_ring_attention_multi_rank(world, causal, zigzag):
+@pytest.mark.parametrize("world,causal,zigzag,S", [(2, True, False, 1024), (4, True, False, 1024),
+                                                   (2, False, False, 1024), (2, True, True, 1024),
+                                                   (4, True, True, 1024), (8, True, False, 2048),
+                                                   (8, True, True, 2048)])
+def test_ring_attention_multi_rank(world, causal, zigzag, S):
     """Contiguous (reference) split, and the zig-zag split (PICO_CP_ZIGZAG=1: rank r holds chunks r and
     2 cp - 1 - r; every rank does equal block work), against whole-sequence attention at the rows each
-    rank holds."""
-    mp.start_processes(_worker, args=(world, _free_port(), causal, zigzag), nprocs=world, join=True,
+    rank holds. cp = 8 (C5's ring size): the 8-step ring loop, and the zig-zag split
+    into 2 cp = 16 chunks, at S = 2048."""
+    mp.start_processes(_worker, args=(world, _free_port(), causal, zigzag, S), nprocs=world, join=True,
                        start_method="spawn")

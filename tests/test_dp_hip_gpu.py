@@ -111,3 +111,22 @@ def test_dp_w2_fusion_toggled_between_micro_batches(tmp_path):
         # the plain path rounds each micro-batch's dW to bf16 before the fp32 accumulate: ~1e-3; a dropped
         # micro-batch would be ~0.3
         assert err < 2e-2, (name, err)
+
+
+def test_dp_w8_rank_data_matches_single_process_sum(tmp_path):
+    """C3 rehearsal at its real world size: eight gloo ranks on one GPU, the product
+    model with fused wgrad into main_grad and the 1/8 pre-scale folded into the syncing GEMMs / norm dw /
+    embedding backward; main_grad must equal 1/8 of a one-process sum over the eight ranks' micro-batches
+    (fp32 summation order only), .grad its bf16 cast bit for bit, and all eight replicas identical."""
+    seeds = [[60 + r] for r in range(8)]
+    w8 = _run(8, seeds, False, tmp_path)
+    w1 = _run(1, [[60 + r for r in range(8)]], False, tmp_path)[0]
+    for r in range(8):
+        for name, (mg, g) in w8[r].items():
+            ref = w1[name][0] / 8
+            err = float((mg - ref).norm() / ref.norm().clamp_min(1e-30))
+            assert err < 4e-6, (r, name, err)
+            assert torch.equal(g, mg.to(torch.bfloat16)), name
+    for r in range(1, 8):
+        for name in w8[0]:
+            assert torch.equal(w8[0][name][0], w8[r][name][0]), (r, name)
