@@ -164,7 +164,8 @@ def main():
     model = build_llama(cfg, device=device, dtype=torch.bfloat16)
     num_params = sum(p.numel() for p in model.parameters())
     if world > 1:
-        model = DataParallelBucket(model)
+        # the bf16 .grad cast (ref data_parallel.py:165) fused into the pico AdamW step (bit-identical)
+        model = DataParallelBucket(model, defer_grad_cast=args.optimizer == "pico")
     # ref train.py:204-209: AdamW(lr), fused when the config's use_fused_adam is set (template default true)
     if args.optimizer == "pico":
         from picotron_amd.optim import AdamW

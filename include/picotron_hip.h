@@ -237,8 +237,10 @@ int pico_sort_ids(const int64_t* ids, int64_t n, int64_t vocab, int64_t* sorted_
 /* ---- AdamW step over a whole parameter list (one launch) ----
  * Replaces torch.optim.AdamW(params, lr, fused=True).step() (ref train.py:13,204-209,235) for bf16
  * parameters with bf16 exp_avg / exp_avg_sq (torch keeps the states in the parameter dtype).
- * tensors: device int64 [n_tensors][4] = (param, grad, exp_avg, exp_avg_sq) addresses; sizes: device
- * int64 [n_tensors] numel; chunks: device int64 [n_chunks][2] = (tensor index, first element), one
+ * tensors: device int64 [n_tensors][5] = (param, grad, exp_avg, exp_avg_sq addresses, grad_is_f32);
+ * grad_is_f32 != 0: grad is an fp32 buffer (DataParallelBucket's averaged main_grad with the bf16 .grad
+ * cast deferred, ref picotron/data_parallel/data_parallel.py:165), rounded to bf16 in register exactly as
+ * pico_cast_f32_bf16 stores it — bit-identical to cast-then-step; sizes: device int64 [n_tensors] numel; chunks: device int64 [n_chunks][2] = (tensor index, first element), one
  * per pico_adamw_chunk_elems() elements of each tensor. step: the step number after increment (>= 1).
  * Same expression order and types as ATen's fused AdamW (decoupled weight decay). */
 int64_t pico_adamw_chunk_elems(void);

@@ -71,8 +71,9 @@ def get_kernels():
 
 class Bucket:
     def __init__(self, params: List[torch.nn.Parameter], grad_data: torch.Tensor, process_group,
-                 grad_out: torch.Tensor = None) -> None:
+                 grad_out: torch.Tensor = None, defer_cast: bool = False) -> None:
         self.params = set(params)
+        self.defer_cast = defer_cast          # the bf16 cast is left to the optimizer (or materialize())
         self.params_with_grad_ready = set()
         self.grad_data = grad_data            # flat fp32 gradients of this bucket
         self.grad_out = grad_out              # flat param-dtype buffer whose views become p.grad
@@ -93,7 +94,7 @@ class Bucket:
         elif self.n_prescaled != len(self.params):
             raise RuntimeError("bucket mixes pre-scaled and unscaled parameters")
         self.handle = dist.all_reduce(self.grad_data, group=self.process_group, async_op=True)
-        if self.grad_out is not None and self.grad_data.is_cuda:
+        if self.grad_out is not None and self.grad_data.is_cuda and not self.defer_cast:
             if self.side_stream is None:
                 self.side_stream = torch.cuda.Stream(device=self.grad_data.device)
             with torch.cuda.stream(self.side_stream):
@@ -115,8 +116,13 @@ class Bucket:
             torch.cuda.current_stream(self.grad_data.device).wait_event(self.cast_done)
         else:
             self.handle.wait()
-            if self.grad_out is not None:
+            if self.grad_out is not None and not self.defer_cast:
                 _kernels.cast(self.grad_data, self.grad_out)
+
+    def materialize(self) -> None:
+        """The deferred fp32 -> bf16 cast, on the current stream (after wait())."""
+        if self.grad_out is not None:
+            _kernels.cast(self.grad_data, self.grad_out)
 
     def mark_param_as_ready(self, param: torch.nn.Parameter, prescaled: bool = False) -> None:
         assert param in self.params and param not in self.params_with_grad_ready, \
@@ -130,8 +136,9 @@ class Bucket:
 
 class BucketManager:
     def __init__(self, params: List[torch.nn.Parameter], process_group, bucket_size: int,
-                 grad_type: torch.dtype = torch.float32) -> None:
+                 grad_type: torch.dtype = torch.float32, defer_cast: bool = False) -> None:
         self.params = list(params)
+        self.defer_cast = defer_cast
         self.device = self.params[0].device
         self.buckets = []
         self.process_group = process_group
@@ -187,7 +194,7 @@ class BucketManager:
             go = torch.empty(n, dtype=pdt, device=self.device)
             self.grad_data_list.append(gd)
             self.grad_out_list.append(go)
-            self.buckets.append(Bucket(buckets_to_params[i], gd, self.process_group, go))
+            self.buckets.append(Bucket(buckets_to_params[i], gd, self.process_group, go, defer_cast=self.defer_cast))
         for param in self.params[::-1]:
             if not param.requires_grad:
                 continue
@@ -206,6 +213,10 @@ class BucketManager:
     def wait(self) -> None:
         for bucket in self.buckets:
             bucket.wait()
+
+    def materialize(self) -> None:
+        for bucket in self.buckets:
+            bucket.materialize()
 
     def mark_param_as_ready(self, param: torch.nn.Parameter, prescaled: bool = False) -> None:
         bucket_idx = self.params_to_bucket_location[param][2]

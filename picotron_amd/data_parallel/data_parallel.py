@@ -56,14 +56,20 @@ class DataParallelNaive(nn.Module):
 
 class DataParallelBucket(nn.Module):
 
-    def __init__(self, module, bucket_cap_mb=25, grad_type=torch.float32):
+    def __init__(self, module, bucket_cap_mb=25, grad_type=torch.float32, defer_grad_cast=False):
+        """ref :62-85. defer_grad_cast (an extension, off by default): after a syncing backward `.grad` is the
+        bucket's bf16 view WITHOUT the fp32 -> bf16 cast of ref :165 having run; picotron_amd.optim.AdamW reads
+        the averaged fp32 main_grad instead and rounds it to bf16 in register exactly as the cast would
+        (bit-identical step, no bf16 .grad write + re-read: 4 B per parameter per step). Anything else that
+        reads `.grad` must call materialize_grads() first."""
         super().__init__()
         self.module = module
         self.require_backward_grad_sync = True
+        self.defer_grad_cast = bool(defer_grad_cast)
         grad_size = 2 if grad_type == torch.bfloat16 else 4
         bucket_size = bucket_cap_mb * 1024 * 1024 // grad_size
         self.bucket_manager = BucketManager(module.parameters(), pgm.process_group_manager.cp_dp_group, bucket_size,
-                                            grad_type)
+                                            grad_type, defer_cast=self.defer_grad_cast)
         self._fused_pass = set()  # params a fused producer accumulated in the running backward pass
         self._pass_cb_set = False
         self.register_backward_hook()
@@ -150,8 +156,23 @@ class DataParallelBucket(nn.Module):
         for p in self.module.parameters():
             if p.requires_grad:
                 p.grad = self.bucket_manager.grad_view(p)
+                if self.defer_grad_cast:  # the optimizer reads main_grad (see __init__)
+                    p._pico_grad_f32 = p.main_grad
+                    p._pico_grad_deferred = True
+
+    def materialize_grads(self):
+        """Run the deferred bf16 cast (defer_grad_cast=True) so `.grad` holds the averaged gradient."""
+        if any(getattr(p, "_pico_grad_deferred", False) for p in self.module.parameters()):
+            self.bucket_manager.materialize()
+            self._clear_deferred()
+
+    def _clear_deferred(self):
+        for p in self.module.parameters():
+            if getattr(p, "_pico_grad_deferred", False):
+                p._pico_grad_deferred = False
 
     def reset(self):
         self.bucket_manager.reset()
+        self._clear_deferred()
         self._end_pass()
         self._post_backward_callback_set = False

@@ -13,6 +13,17 @@ import torch
 from . import _lib
 
 
+def _deferred_grad(p):
+    """The fp32 main_grad the step reads instead of .grad when DataParallelBucket(defer_grad_cast=True) left
+    the bf16 .grad cast to the optimizer (the kernel rounds it to bf16 in register, as the cast would)."""
+    g32 = getattr(p, "_pico_grad_f32", None)
+    if g32 is None or not getattr(p, "_pico_grad_deferred", False):
+        return None
+    if g32.dtype != torch.float32 or not g32.is_contiguous() or g32.shape != p.shape:
+        raise ValueError("picotron_amd.optim.AdamW: deferred-cast gradient must be a contiguous fp32 main_grad")
+    return g32
+
+
 class AdamW(torch.optim.Optimizer):
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, amsgrad=False, *,
                  maximize=False, foreach=None, capturable=False, differentiable=False, fused=None):
@@ -39,15 +50,19 @@ class AdamW(torch.optim.Optimizer):
             sizes = torch.tensor([p.numel() for p in params], dtype=torch.int64)
             chunks = torch.tensor([(i, c) for i, p in enumerate(params) for c in range(0, p.numel(), chunk)],
                                   dtype=torch.int64).reshape(-1, 2)
-            ent = {"tens": torch.empty((len(params), 4), dtype=torch.int64, device=dev), "sizes": sizes.to(dev),
+            ent = {"tens": torch.empty((len(params), 5), dtype=torch.int64, device=dev), "sizes": sizes.to(dev),
                    "chunks": chunks.to(dev), "n_chunks": chunks.shape[0], "ptrs": None, "turn": 0,
-                   "host": [torch.empty((len(params), 4), dtype=torch.int64).pin_memory() for _ in range(2)],
+                   "host": [torch.empty((len(params), 5), dtype=torch.int64).pin_memory() for _ in range(2)],
                    "done": [None, None]}
             if len(self._tables) > 64:  # parameter sets keep changing (step counts diverging): keep the map small
                 self._tables.clear()
             self._tables[key] = ent
-        ptrs = [(p.data_ptr(), p.grad.data_ptr(), self.state[p]["exp_avg"].data_ptr(),
-                 self.state[p]["exp_avg_sq"].data_ptr()) for p in params]
+        ptrs = []
+        for p in params:
+            g32 = _deferred_grad(p)
+            ptrs.append((p.data_ptr(), (g32 if g32 is not None else p.grad).data_ptr(),
+                         self.state[p]["exp_avg"].data_ptr(), self.state[p]["exp_avg_sq"].data_ptr(),
+                         0 if g32 is None else 1))
         if ptrs != ent["ptrs"]:
             i = ent["turn"]
             if ent["done"][i] is not None:  # this staging buffer may still be feeding its previous copy

@@ -130,3 +130,66 @@ def test_dp_w8_rank_data_matches_single_process_sum(tmp_path):
     for r in range(1, 8):
         for name in w8[0]:
             assert torch.equal(w8[0][name][0], w8[r][name][0]), (r, name)
+
+
+def _adam_worker(rank, world, port, defer, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from picotron_amd import process_group_manager as pgm
+    from picotron_amd.data_parallel.data_parallel import DataParallelBucket
+    from picotron_amd.model import LlamaConfig, build_llama
+    from picotron_amd.optim import AdamW
+    from picotron_amd.train import _micro_batch
+
+    pgm.setup_process_group_manager(tp_size=1, cp_size=1, pp_size=1, dp_size=world)
+    cfg = LlamaConfig(hidden_size=256, intermediate_size=512, num_attention_heads=4, num_key_value_heads=2,
+                      num_hidden_layers=2, vocab_size=512, max_position_embeddings=64)
+    torch.manual_seed(42)
+    model = build_llama(cfg, device="cuda:0")
+    with torch.no_grad():
+        g = torch.Generator().manual_seed(7)
+        model.final_proj.weight.copy_(torch.randn(model.final_proj.weight.shape, generator=g) * 0.02)
+    model = DataParallelBucket(model, defer_grad_cast=defer)
+    opt = AdamW(model.parameters(), lr=1e-3)
+    for step in range(2):
+        opt.zero_grad()
+        batches = _batches(70 + 10 * step + rank, GRAD_ACC)
+        for i, (x, y) in enumerate(batches):
+            model.require_backward_grad_sync = i == len(batches) - 1
+            _micro_batch(model, x.cuda(), y.cuda(), GRAD_ACC)
+        if defer:
+            assert all(p._pico_grad_deferred for p in model.module.parameters())
+        opt.step()
+        model.reset()
+    torch.cuda.synchronize()
+    res = {name: (p.detach().cpu().clone(), opt.state[p]["exp_avg"].cpu().clone(), opt.state[p]["exp_avg_sq"].cpu().clone())
+           for name, p in model.module.named_parameters()}
+    if defer:  # materialize_grads() gives the .grad the eager cast would have written
+        for i, (x, y) in enumerate(_batches(99 + rank, 1)):
+            model.require_backward_grad_sync = True
+            _micro_batch(model, x.cuda(), y.cuda(), 1)
+        model.materialize_grads()
+        torch.cuda.synchronize()
+        for p in model.module.parameters():
+            assert torch.equal(p.grad, p.main_grad.to(torch.bfloat16))
+    torch.save(res, os.path.join(out_dir, f"{'d' if defer else 'c'}{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_adamw_reads_deferred_fp32_grads_bit_exact(tmp_path):
+    """DataParallelBucket(defer_grad_cast=True) skips the fp32 -> bf16
+    .grad cast (ref picotron/data_parallel/data_parallel.py:165) and pico_adamw_bf16 reads the averaged fp32
+    main_grad, rounding in register: two AdamW steps at W = 2 (gloo) leave parameters and both moments bit for
+    bit equal to the eager cast + step."""
+    for defer in (False, True):
+        mp.start_processes(_adam_worker, args=(2, _free_port(), defer, str(tmp_path)), nprocs=2, join=True,
+                           start_method="spawn")
+    for r in range(2):
+        c = torch.load(tmp_path / f"c{r}.pt", weights_only=True)
+        d = torch.load(tmp_path / f"d{r}.pt", weights_only=True)
+        for name in c:
+            for a, b in zip(c[name], d[name]):
+                assert torch.equal(a, b), name
