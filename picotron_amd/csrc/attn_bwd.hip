@@ -859,9 +859,13 @@ int launch_bwd(const pico_attn_args* a, hipStream_t s) {
 }  // namespace
 
 // Shared argument validation for forward and backward.
-// split backward for head_dim 64 (attn_bwd_split.hip); PICO_BWD_SPLIT_D64=0 builds the fused form instead
+// split backward for head_dim 64 (attn_bwd_split.hip) and 128 (attn_bwd_split_d128.hip); PICO_BWD_SPLIT_D64=0 /
+// PICO_BWD_SPLIT_D128=0 build the fused form with per-key-block dQ slabs instead
 #ifndef PICO_BWD_SPLIT_D64
 #define PICO_BWD_SPLIT_D64 1
+#endif
+#ifndef PICO_BWD_SPLIT_D128
+#define PICO_BWD_SPLIT_D128 1
 #endif
 int64_t pico_attn_bwd_split_workspace(const pico_attn_args* a);
 int pico_attn_bwd_split(const pico_attn_args* a, hipStream_t s);
@@ -891,6 +895,7 @@ int64_t pico_attn_args_size(void) { return (int64_t)sizeof(pico_attn_args); }
 
 int64_t pico_attn_bwd_workspace_bytes(const pico_attn_args* a) {
   if (PICO_BWD_SPLIT_D64 && a->head_dim == 64) return pico_attn_bwd_split_workspace(a);
+  if (PICO_BWD_SPLIT_D128 && a->head_dim == 128) return pico_attn_bwd_split_workspace(a);
   // lse2, delta [B*Hq*Sq_pad] fp32 + one fp32 dQ partial slab [B, Sq, Hq, D] per 256-key block of a group
   // (at most PICO_BWD_KB_CAP; grouped: + an fp32 dQ accumulator unless the caller's dQ is fp32)
   const int64_t nkb = (a->seqlen_k + BK - 1) / BK;
@@ -922,6 +927,7 @@ int pico_attn_bwd(const pico_attn_args* a, void* stream) {
   if (a->batch == 0 || a->seqlen_q == 0 || a->heads_q == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   if (a->head_dim == 64) return PICO_BWD_SPLIT_D64 ? pico_attn_bwd_split(a, s) : launch_bwd<64>(a, s);
+  if (PICO_BWD_SPLIT_D128) return pico_attn_bwd_split(a, s);
   return launch_bwd<128>(a, s);
 }
 

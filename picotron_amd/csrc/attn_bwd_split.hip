@@ -1,4 +1,4 @@
-// Flash-attention backward for gfx950, split form (head_dim 64): a query-major dQ kernel and a
+// Flash-attention backward for gfx950, split form (head_dim 64 here; 128 in attn_bwd_split_d128.hip): a query-major dQ kernel and a
 // key-major dK/dV kernel instead of one kernel whose dQ needs a cross-workgroup reduction.
 //
 // Replaces flash-attn's backward of flash_attn_func (ref picotron/model.py:36) and the ring block
@@ -100,6 +100,9 @@ constexpr int64_t STAMP_BYTES = PICO_BWDKV_STAMP ? 8 * STAMP_T * STAMP_P * 8
 template <int D>
 struct QCfg {
   static constexpr int KS = D / 16, DT = D / 32, CPR = D / 8, RB = 2 * D;
+  // workgroups per CU the register budget is sized for: D = 128 holds 2x the fragments and dQ accumulators
+  // (≈ 290 registers with the AGPRs its own translation unit may use: one workgroup per CU)
+  static constexpr int MINB = D == 64 ? PICO_BWDQ_MINB : 1;
   static constexpr int IMG = KT * RB;          // one K (or V) tile image (lds_off<D> layout)
   static constexpr int SLOT = 2 * IMG;         // K | V
   static constexpr int NBUF = PICO_BWDQ_NBUF;  // ring slots; prefetch distance NBUF - 1
@@ -156,7 +159,7 @@ PICO_DEV void tr_offsets(int lane, unsigned (&tro)[D / 32][2]) {
 // dQ kernel (query-major)
 // ------------------------------------------------------------------------------------------------
 template <int D, bool CAUSAL>
-__global__ __launch_bounds__(256, PICO_BWDQ_MINB) void attn_bwd_q_kernel(const pico_attn_args a, float scale, float scale_log2,
+__global__ __launch_bounds__(256, QCfg<D>::MINB) void attn_bwd_q_kernel(const pico_attn_args a, float scale, float scale_log2,
                                                              float* __restrict__ lse2_g, float* __restrict__ delta_g,
                                                              int sq_pad, unsigned long long* __restrict__ stamp_out,
                                                              int nfront) {
@@ -989,6 +992,7 @@ int64_t split_lsd_floats(const pico_attn_args* a) {
 // dK/dV workgroups per CU (see PICO_KV_MINB): 3 for causal grids, 2 for non-causal ones (whose mask-free
 // body does not fit 168 VGPRs without spills either)
 int kv_minb(const pico_attn_args* a) {
+  if (a->head_dim == 128) return 1;  // ≈ 340 registers (its own translation unit, AGPRs allowed)
   if (PICO_KV_MINB) return PICO_KV_MINB;
   return a->causal ? 3 : 2;
 }
@@ -1018,7 +1022,8 @@ int q_front(const pico_attn_args* a) {
   const int nmb = (int)((a->seqlen_q + QB - 1) / QB);
   if (PICO_BWDQ_FRONT >= 0) return PICO_BWDQ_FRONT < nmb ? PICO_BWDQ_FRONT : nmb;
   const int64_t nbh = a->batch * a->heads_q;
-  const int64_t first = (int64_t)pico_num_cus() * PICO_BWDQ_MINB / (nbh > 0 ? nbh : 1);  // groups resident at once
+  const int64_t first = (int64_t)pico_num_cus() * (a->head_dim == 64 ? QCfg<64>::MINB : QCfg<128>::MINB) /
+                        (nbh > 0 ? nbh : 1);  // groups resident at once
   return first < nmb ? (int)(nmb - first) : 0;
 }
 
@@ -1036,9 +1041,8 @@ int kv_front(const pico_attn_args* a, int hsplit) {
   return first < nkb ? (int)(nkb - first) : 0;
 }
 
-template <bool CAUSAL>
+template <int D, bool CAUSAL>
 int launch_split(const pico_attn_args* a, hipStream_t s) {
-  constexpr int D = 64;
   const int sq_pad = split_sq_pad(a);
   float* lse2 = (float*)a->workspace;
   float* delta = lse2 + split_lsd_floats(a);
@@ -1055,7 +1059,9 @@ int launch_split(const pico_attn_args* a, hipStream_t s) {
   const int64_t nblk = (int64_t)nkb * a->batch * a->heads_kv * hsplit;
   if (nblk == 0) return 0;
   unsigned long long* stamps = (unsigned long long*)((char*)a->workspace + pico_attn_bwd_split_workspace(a) - STAMP_BYTES);
-  if (CAUSAL && kv_minb(a) == 3) {
+  if constexpr (D == 128) {
+    PICO_TRY(pico_launch(PICO_K_ATTN_BWD_KV, "attn_bwd_kv", attn_bwd_kv_kernel<D, CAUSAL, 1>, dim3((int)nblk), dim3(KNW * 64), 0, s, *a, a->softmax_scale, sl2, lse2, delta, sq_pad, hsplit, dkv_part, stamps, kv_front(a, hsplit)));
+  } else if (CAUSAL && kv_minb(a) == 3) {
     PICO_TRY(pico_launch(PICO_K_ATTN_BWD_KV, "attn_bwd_kv", attn_bwd_kv_kernel<D, CAUSAL, 3>, dim3((int)nblk), dim3(KNW * 64), 0, s, *a, a->softmax_scale, sl2, lse2, delta, sq_pad, hsplit, dkv_part, stamps, kv_front(a, hsplit)));
   } else {
     PICO_TRY(pico_launch(PICO_K_ATTN_BWD_KV, "attn_bwd_kv", attn_bwd_kv_kernel<D, CAUSAL, 2>, dim3((int)nblk), dim3(KNW * 64), 0, s, *a, a->softmax_scale, sl2, lse2, delta, sq_pad, hsplit, dkv_part, stamps, kv_front(a, hsplit)));
@@ -1071,12 +1077,25 @@ int launch_split(const pico_attn_args* a, hipStream_t s) {
 
 // workspace of the split backward: [lse2 | delta] each [B*Hq][Sq_pad32] fp32 (+ fp32 dK/dV partials when
 // a small grid splits key blocks): O(S), independent of the number of key blocks
+#ifndef PICO_SPLIT_D128_TU
 int64_t pico_attn_bwd_split_workspace(const pico_attn_args* a) {
   const int hs = kv_hsplit(a);
   const int64_t dkv = hs > 1 ? 2 * hs * a->batch * a->seqlen_k * a->heads_kv * a->head_dim : 0;
   return (2 * split_lsd_floats(a) + dkv) * 4 + STAMP_BYTES;
 }
+#endif
+
+#ifndef PICO_SPLIT_D128_TU
+int pico_attn_bwd_split_d128(const pico_attn_args* a, hipStream_t s);  // attn_bwd_split_d128.hip
 
 int pico_attn_bwd_split(const pico_attn_args* a, hipStream_t s) {
-  return a->causal ? launch_split<true>(a, s) : launch_split<false>(a, s);
+  if (a->head_dim == 128) return pico_attn_bwd_split_d128(a, s);
+  return a->causal ? launch_split<64, true>(a, s) : launch_split<64, false>(a, s);
 }
+#else
+// head_dim 128: its own translation unit (built without -amdgpu-mfma-vgpr-form: the D = 128 dK / dV and dQ
+// accumulators need the AGPR half of the register file)
+int pico_attn_bwd_split_d128(const pico_attn_args* a, hipStream_t s) {
+  return a->causal ? launch_split<128, true>(a, s) : launch_split<128, false>(a, s);
+}
+#endif

@@ -203,8 +203,13 @@ constexpr int PREV_COLS = 16;  // column slots per workgroup (cpw <= 16)
 // dw partial per workgroup (deterministic two-stage reduction, no atomics).
 // FULL: cols == MAXC * 512 (every lane chunk in range: no per-chunk predicates, which otherwise
 // make hipcc spill). NW waves per workgroup (16 up to 1024 columns, 8 up to 2048, 4 above — the
-// most that fit without spilling), one row per wave per pass, at most one workgroup per CU; the
-// per-wave dw partials accumulate in LDS and the workgroup's sum is one fp32 row per CU.
+// most that fit without spilling), R rows per wave per pass (every load of the R rows in flight before
+// the first use; R = 2 measured 13.33 vs 13.06 us for R = 1 on the SmolLM chained launch, so 1 by default),
+// at most one workgroup per CU; the per-wave dw partials accumulate in LDS and the workgroup's sum is one
+// fp32 row per CU. The weight chunks are loaded once per wave (loop-invariant).
+#ifndef PICO_RMS_BWD_R
+#define PICO_RMS_BWD_R 1
+#endif
 template <int MAXC, int NW, bool FULL, bool RES>
 __global__ __launch_bounds__(NW * 64) void rmsnorm_bwd_kernel(const bf16_t* __restrict__ dy,
                                                               const bf16_t* __restrict__ dres,
@@ -212,11 +217,14 @@ __global__ __launch_bounds__(NW * 64) void rmsnorm_bwd_kernel(const bf16_t* __re
                                                               const float* __restrict__ rstd, bf16_t* __restrict__ dx,
                                                               float* __restrict__ dw_part, int64_t rows, int cols,
                                                               const DwPrev prev) {
+  // R rows only where they fit without spilling (16-wave MAXC 2 and the predicated MAXC 4 forms do not)
+  constexpr int R = (MAXC == 1 || MAXC == 8 || (MAXC == 4 && FULL)) ? PICO_RMS_BWD_R : 1;
   __shared__ float red[NW * MAXC * 512];  // per-wave dw partial rows (accumulated in LDS, not registers)
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   // chained dw of the previous call: this thread's partial rows of one column slot, loaded first (in flight
-  // during the row loop); slot c = t % 16, row group g = t / 16, rows g, g + NG, ...
+  // during the row loop); slot c = t % 16, row group g = t / 16, rows g, g + NG, ... — and the current value
+  // of the target column for the in-place modes (its read is off the kernel's tail too)
   constexpr int NG = NW * 64 / PREV_COLS, PR = 256 / NG;  // prev.nb <= 256 (host check)
   float pv[PR];
   const int pcs = threadIdx.x % PREV_COLS, pg = threadIdx.x / PREV_COLS;
@@ -227,61 +235,76 @@ __global__ __launch_bounds__(NW * 64) void rmsnorm_bwd_kernel(const bf16_t* __re
     const int pr = pg + NG * k;
     pv[k] = (pok && pr < prev.nb) ? prev.part[(int64_t)pr * prev.cols + pcol] : 0.f;
   }
+  float pold = 0.f;
+  if (pok && pg == 0 && prev.mode != 0)
+    pold = prev.mode == 1 ? bf2f(((const bf16_t*)prev.dw)[pcol]) : ((const float*)prev.dw)[pcol];
   float* myred = red + wid * MAXC * 512 + lane * 8;  // chunk c at + 512 c
 #pragma unroll
   for (int c = 0; c < MAXC; ++c) {
     *reinterpret_cast<f32x4*>(myred + 512 * c) = (f32x4)0.f;
     *reinterpret_cast<f32x4*>(myred + 512 * c + 4) = (f32x4)0.f;
   }
-  const bf16_t* wl = w + lane * 8;
+  u16x8 wv[MAXC];  // loop-invariant
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c)
+    if (FULL || (c * 64 + lane) * 8 < cols) wv[c] = *reinterpret_cast<const u16x8*>(w + lane * 8 + 512 * c);
+  const int64_t stride = (int64_t)gridDim.x * NW;
 #pragma unroll 1
-  for (int64_t row = (int64_t)blockIdx.x * NW + wid; row < rows; row += (int64_t)gridDim.x * NW) {
-    const float rs = rstd[row];
-    const int64_t ro = row * cols + lane * 8;  // this lane's first element of the row; chunk c at + 512 c
-    const bf16_t* xr = x + ro;
-    const bf16_t* dr = dy + ro;
-    const bf16_t* rr = RES ? dres + ro : nullptr;
-    u16x8 xv[MAXC], dv[MAXC], rv[MAXC], wv[MAXC];
+  for (int64_t row0 = (int64_t)blockIdx.x * NW + wid; row0 < rows; row0 += R * stride) {
+    u16x8 xv[R][MAXC], dv[R][MAXC], rv[R][MAXC];
+    float rs[R];
 #pragma unroll
-    for (int c = 0; c < MAXC; ++c) {  // every load of the row in flight before any use (w: L1/L2 hits)
-      if (FULL || (c * 64 + lane) * 8 < cols) {
-        xv[c] = *reinterpret_cast<const u16x8*>(xr + 512 * c);
-        dv[c] = *reinterpret_cast<const u16x8*>(dr + 512 * c);
-        if constexpr (RES) rv[c] = *reinterpret_cast<const u16x8*>(rr + 512 * c);
-        wv[c] = *reinterpret_cast<const u16x8*>(wl + 512 * c);
+    for (int r = 0; r < R; ++r) {  // every load of the R rows in flight before any use
+      const int64_t row = row0 + r * stride;
+      if (r == 0 || row < rows) {  // wave-uniform
+        rs[r] = rstd[row];
+        const int64_t ro = row * cols + lane * 8;  // this lane's first element of the row; chunk c at + 512 c
+#pragma unroll
+        for (int c = 0; c < MAXC; ++c) {
+          if (FULL || (c * 64 + lane) * 8 < cols) {
+            xv[r][c] = *reinterpret_cast<const u16x8*>(x + ro + 512 * c);
+            dv[r][c] = *reinterpret_cast<const u16x8*>(dy + ro + 512 * c);
+            if constexpr (RES) rv[r][c] = *reinterpret_cast<const u16x8*>(dres + ro + 512 * c);
+          }
+        }
       }
     }
-    float dot = 0.f;
 #pragma unroll
-    for (int c = 0; c < MAXC; ++c) {
-      if (FULL || (c * 64 + lane) * 8 < cols) {
-        f32x4 a = *reinterpret_cast<const f32x4*>(myred + 512 * c);
-        f32x4 bq = *reinterpret_cast<const f32x4*>(myred + 512 * c + 4);
+    for (int r = 0; r < R; ++r) {
+      const int64_t row = row0 + r * stride;
+      if (r > 0 && row >= rows) break;  // wave-uniform
+      float dot = 0.f;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float xh = bf2f(xv[c][j]) * rs, d = bf2f(dv[c][j]);
-          if (j < 4) a[j] += d * xh;
-          else bq[j - 4] += d * xh;
-          dot += d * bf2f(wv[c][j]) * xh;
+      for (int c = 0; c < MAXC; ++c) {
+        if (FULL || (c * 64 + lane) * 8 < cols) {
+          f32x4 a = *reinterpret_cast<const f32x4*>(myred + 512 * c);
+          f32x4 bq = *reinterpret_cast<const f32x4*>(myred + 512 * c + 4);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float xh = bf2f(xv[r][c][j]) * rs[r], d = bf2f(dv[r][c][j]);
+            if (j < 4) a[j] += d * xh;
+            else bq[j - 4] += d * xh;
+            dot += d * bf2f(wv[c][j]) * xh;
+          }
+          *reinterpret_cast<f32x4*>(myred + 512 * c) = a;
+          *reinterpret_cast<f32x4*>(myred + 512 * c + 4) = bq;
         }
-        *reinterpret_cast<f32x4*>(myred + 512 * c) = a;
-        *reinterpret_cast<f32x4*>(myred + 512 * c + 4) = bq;
       }
-    }
-    dot = wave_sum(dot) / (float)cols;
-    bf16_t* dxr = dx + ro;
+      dot = wave_sum(dot) / (float)cols;
+      bf16_t* dxr = dx + row * cols + lane * 8;
 #pragma unroll
-    for (int c = 0; c < MAXC; ++c) {
-      if (FULL || (c * 64 + lane) * 8 < cols) {
-        u16x8 o;
+      for (int c = 0; c < MAXC; ++c) {
+        if (FULL || (c * 64 + lane) * 8 < cols) {
+          u16x8 o;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float xh = bf2f(xv[c][j]) * rs;
-          float v = rs * (bf2f(dv[c][j]) * bf2f(wv[c][j]) - xh * dot);
-          if constexpr (RES) v += bf2f(rv[c][j]);
-          o[j] = f2bf(v);
+          for (int j = 0; j < 8; ++j) {
+            const float xh = bf2f(xv[r][c][j]) * rs[r];
+            float v = rs[r] * (bf2f(dv[r][c][j]) * bf2f(wv[c][j]) - xh * dot);
+            if constexpr (RES) v += bf2f(rv[r][c][j]);
+            o[j] = f2bf(v);
+          }
+          *reinterpret_cast<u16x8*>(dxr + 512 * c) = o;
         }
-        *reinterpret_cast<u16x8*>(dxr + 512 * c) = o;
       }
     }
   }
@@ -297,21 +320,23 @@ __global__ __launch_bounds__(NW * 64) void rmsnorm_bwd_kernel(const bf16_t* __re
     float s = 0.f;
 #pragma unroll
     for (int k = 0; k < PR; ++k) s += pv[k];  // rows ascending
+    // the wave's four row groups of one column slot (lanes pcs, +16, +32, +48): ((g0 + g1) + (g2 + g3))
+    s += __shfl_xor(s, 16);
+    s += __shfl_xor(s, 32);
     __syncthreads();  // every thread past its reads of red
-    red[pg * PREV_COLS + pcs] = s;
+    if (lane < PREV_COLS) red[wid * PREV_COLS + lane] = s;
     __syncthreads();
     if (threadIdx.x < prev.cpw && blockIdx.x * prev.cpw + (int)threadIdx.x < prev.cols) {
       const int col = blockIdx.x * prev.cpw + threadIdx.x;
       float t = 0.f;
-      for (int g = 0; g < NG; ++g) t += red[g * PREV_COLS + threadIdx.x];  // groups ascending: fixed order
+#pragma unroll
+      for (int g = 0; g < NW; ++g) t += red[g * PREV_COLS + threadIdx.x];  // waves ascending: fixed order
       if (prev.mode == 0) {
         ((bf16_t*)prev.dw)[col] = f2bf(t);
       } else if (prev.mode == 1) {
-        bf16_t* q = (bf16_t*)prev.dw + col;
-        *q = f2bf(bf2f(*q) + t);
+        ((bf16_t*)prev.dw)[col] = f2bf(pold + t);
       } else {
-        float* q = (float*)prev.dw + col;
-        *q = (*q + t) * prev.scale;
+        ((float*)prev.dw)[col] = (pold + t) * prev.scale;
       }
     }
   }

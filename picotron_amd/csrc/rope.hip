@@ -12,22 +12,37 @@
 
 namespace {
 
+// n / d for 0 <= n < 2^31 by a multiply-high (round-up method; m and l precomputed on the host): the rope
+// thread's index decomposition otherwise costs three 32-bit integer divisions (~40 VALU each), a sizeable
+// share of a kernel that issues four 16-byte loads per thread
+struct FastDiv {
+  unsigned d, m, l;
+};
+FastDiv make_fastdiv(unsigned d) {
+  FastDiv f;
+  f.d = d;
+  f.l = 0;
+  while ((1ull << f.l) < d) ++f.l;
+  f.m = (unsigned)((((1ull << 32) * ((1ull << f.l) - d)) / d) + 1);
+  return f;
+}
+PICO_DEV unsigned fdiv(unsigned n, const FastDiv& f) { return (__umulhi(n, f.m) + n) >> f.l; }
+
 __global__ __launch_bounds__(256) void rope_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ out,
                                                    const bf16_t* __restrict__ cosp, const bf16_t* __restrict__ sinp,
-                                                   int64_t total, int S, int H, int half, int64_t xs0, int64_t xs1,
-                                                   int64_t xs2, int64_t os0, int64_t os1, int64_t os2, int64_t cs,
-                                                   float sign) {
-  const int vpr = half / 8;  // vectors of 8 pairs per (b, s, h) row
+                                                   int64_t total, FastDiv fv, FastDiv fh, FastDiv fs, int half,
+                                                   int64_t xs0, int64_t xs1, int64_t xs2, int64_t os0, int64_t os1,
+                                                   int64_t os2, int64_t cs, float sign) {
   for (unsigned t = blockIdx.x * 256 + threadIdx.x; t < (unsigned)total; t += gridDim.x * 256) {
-    const int vi = (int)(t % (unsigned)vpr);
-    unsigned r = t / (unsigned)vpr;
-    const int h = (int)(r % (unsigned)H);
-    r /= (unsigned)H;
-    const int s = (int)(r % (unsigned)S);
-    const int64_t b = r / (unsigned)S;
+    const unsigned r0 = fdiv(t, fv);  // (b, s, h) row; vector vi of 8 pairs within it
+    const int vi = (int)(t - r0 * fv.d);
+    const unsigned r1 = fdiv(r0, fh);
+    const int h = (int)(r0 - r1 * fh.d);
+    const unsigned b = fdiv(r1, fs);
+    const int s = (int)(r1 - b * fs.d);
     const int i = vi * 8;
-    const bf16_t* xp = x + b * xs0 + (int64_t)s * xs1 + (int64_t)h * xs2 + i;
-    bf16_t* op = out + b * os0 + (int64_t)s * os1 + (int64_t)h * os2 + i;
+    const bf16_t* xp = x + (int64_t)b * xs0 + (int64_t)s * xs1 + (int64_t)h * xs2 + i;
+    bf16_t* op = out + (int64_t)b * os0 + (int64_t)s * os1 + (int64_t)h * os2 + i;
     const u16x8 x1 = *reinterpret_cast<const u16x8*>(xp);
     const u16x8 x2 = *reinterpret_cast<const u16x8*>(xp + half);
     const u16x8 c = *reinterpret_cast<const u16x8*>(cosp + (int64_t)s * cs + i);
@@ -67,9 +82,9 @@ extern "C" int pico_rope(const void* x, void* out, const void* cos, const void* 
   hipStream_t s = (hipStream_t)stream;
   int64_t nb = (total + 255) / 256;
   if (nb > 8192) nb = 8192;
-  PICO_TRY(pico_launch(PICO_K_ROPE, "rope", rope_kernel, dim3((int)nb), dim3(256), 0, s, (const bf16_t*)x, (bf16_t*)out, (const bf16_t*)cos,
-                                                  (const bf16_t*)sin, total, (int)seqlen, (int)heads,
-                                                  (int)(head_dim / 2), xst[0], xst[1], xst[2], ost[0], ost[1], ost[2],
-                                                  cs_stride, conjugate ? -1.f : 1.f));
+  PICO_TRY(pico_launch(PICO_K_ROPE, "rope", rope_kernel, dim3((int)nb), dim3(256), 0, s, (const bf16_t*)x, (bf16_t*)out,
+                       (const bf16_t*)cos, (const bf16_t*)sin, total, make_fastdiv((unsigned)(head_dim / 16)),
+                       make_fastdiv((unsigned)heads), make_fastdiv((unsigned)seqlen), (int)(head_dim / 2), xst[0], xst[1],
+                       xst[2], ost[0], ost[1], ost[2], cs_stride, conjugate ? -1.f : 1.f));
   return 0;
 }

@@ -52,12 +52,26 @@ def main(iters=50):
         y, res = ops.rms_norm(x, w, 1e-5, residual=r, prenorm=True)
         torch.autograd.backward([y, res], [torch.ones_like(y), torch.ones_like(res)])
 
+    dy2 = torch.randn(T, H, dtype=bf, device=dev)
+    rstd = torch.rand(T, dtype=torch.float32, device=dev) + 0.5
+    dxc = torch.empty(T, H, dtype=bf, device=dev)
+    nb = int(L.load().pico_rmsnorm_bwd_partial_rows(T, H))
+    ws_a = torch.zeros(nb, H, dtype=torch.float32, device=dev)
+    ws_b = torch.zeros(nb, H, dtype=torch.float32, device=dev)
+    mg_prev = torch.zeros(H, dtype=torch.float32, device=dev)
+
+    def run_norm_chain():  # the in-step form: reduce the previous norm's partial rows (fp32 main_grad, mode 2)
+        L.check(L.load().pico_rmsnorm_bwd_chain(
+            L.ptr(dy2), L.ptr(r), L.ptr(x), L.ptr(w), L.ptr(rstd), L.ptr(dxc), None, 2, 1.0, L.ptr(ws_a), T, H, 0,
+            L.ptr(ws_b), nb, H, L.ptr(mg_prev), 2, 1.0, L.stream_of(x)), "pico_rmsnorm_bwd_chain")
+
     def run_norm_t():
         ops._RMSNormFn.apply(x.detach(), r.detach(), w.detach(), 1e-5, True, True)
 
     cases = [
         ("rmsnorm", run_norm, [L.K_RMSNORM_FWD, L.K_RMSNORM_BWD, L.K_RMSNORM_DW]),
         ("rmsnorm_t", run_norm_t, [L.K_RMSNORM_FWD]),
+        ("rmsnorm_chain", run_norm_chain, [L.K_RMSNORM_BWD]),
         ("rope", lambda: ops._rope_launch(qkv[:, :, :2 * NH], qkv[:, :, :2 * NH], cos, sin, False), [L.K_ROPE]),
         ("swiglu", lambda: (ops._swiglu_fwd(gu, gu[:, I:], h, T, I, 2 * I, I),
                             ops._swiglu_bwd(dh, gu, gu[:, I:], dgu, dgu[:, I:], T, I, 2 * I, I)),
@@ -89,7 +103,7 @@ def main(iters=50):
         for k in kids:
             ms, n = L.prof_collect(k)
             us = 1e3 * ms / max(n, 1)
-            out = {"kernel": L.KERNEL_NAMES[k] + ("" if k not in (L.K_TRANSPOSE,) and name not in ("rmsnorm_t", "swiglu_t") else ":" + name), "avg_us": round(us, 2), "launches": n}
+            out = {"kernel": L.KERNEL_NAMES[k] + ("" if k not in (L.K_TRANSPOSE,) and name not in ("rmsnorm_t", "swiglu_t", "rmsnorm_chain") else ":" + name), "avg_us": round(us, 2), "launches": n}
             if k in work:
                 out["GB_s"] = round(work[k] / (us * 1e-6) / 1e9, 1)
                 out["frac_of_8TBs"] = round(out["GB_s"] / 8000, 3)

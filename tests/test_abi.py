@@ -81,19 +81,16 @@ def test_workspace_sizes(lib):
     a.heads_kv = 32
     a.batch, a.seqlen_q, a.seqlen_k = 1, 16384, 16384
     assert lib.pico_attn_bwd_workspace_bytes(ctypes.byref(a)) == 2 * 32 * 16384 * 4
-    # head_dim 128 keeps the fused form: + one fp32 dQ partial slab per 256-key block (+ 64 trash floats)
+    # head_dim 128 runs the split backward too: O(S) LSE / delta, no dQ slabs. C4 per-rank
+    # shape: 8 key blocks x B 2 x 16 heads = 256 workgroups (one per CU at D = 128) -> no tile-list split
     a.batch, a.seqlen_q, a.seqlen_k, a.heads_q, a.heads_kv, a.head_dim = 2, 1024, 1024, 16, 16, 128
-    assert lib.pico_attn_bwd_workspace_bytes(ctypes.byref(a)) == 2 * 2 * 16 * 1024 * 4 + 4 * (2 * 1024 * 16 * 128 * 4) + 256 \
-        + 2 * 2 * 2 * 1024 * 16 * 128 * 4  # B 2 x 16 heads x 4 key blocks = 128 workgroups: dK/dV split 2 ways
-    # (one launch fills the 256 CUs once; GQA twice: 32/8 heads -> 4 x 2 x 8 = 64 workgroups split 8 ways)
+    assert lib.pico_attn_bwd_workspace_bytes(ctypes.byref(a)) == 2 * 2 * 16 * 1024 * 4
+    # GQA 32/8: 128 workgroups -> tile lists split 2 ways, + fp32 dK/dV partials [2][2][B, S, Hkv, D]
     a.heads_q, a.heads_kv = 32, 8
-    assert lib.pico_attn_bwd_workspace_bytes(ctypes.byref(a)) == 2 * 2 * 32 * 1024 * 4 + 4 * (2 * 1024 * 32 * 128 * 4) + 256 \
-        + 2 * 8 * 2 * 1024 * 8 * 128 * 4
-    a.heads_q, a.heads_kv = 16, 16
-    # head_dim 128 past 8 key blocks: slabs bounded at 8 (+ an fp32 dQ accumulator), not one per block
+    assert lib.pico_attn_bwd_workspace_bytes(ctypes.byref(a)) == 2 * 2 * 32 * 1024 * 4 + 2 * 2 * 2 * 1024 * 8 * 128 * 4
+    # O(S) at long sequences
     a.batch, a.seqlen_q, a.seqlen_k, a.heads_q, a.heads_kv = 1, 16384, 16384, 32, 32
-    slab = 16384 * 32 * 128 * 4
-    assert lib.pico_attn_bwd_workspace_bytes(ctypes.byref(a)) == 2 * 32 * 16384 * 4 + (8 + 1) * slab + 256
+    assert lib.pico_attn_bwd_workspace_bytes(ctypes.byref(a)) == 2 * 32 * 16384 * 4
 
 
 def test_ops_fail_loudly_without_hip_tensors(lib):

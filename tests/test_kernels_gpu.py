@@ -69,16 +69,16 @@ def test_rmsnorm_shapes(rows, cols):
         assert rel_l2(wr.grad.cpu(), dw) < 4e-3
 
 
-@pytest.mark.parametrize("cols", [2048, 4096])
-def test_rmsnorm_chained_dw(monkeypatch, cols):
+@pytest.mark.parametrize("rows,cols", [(512, 2048), (512, 4096), (5000, 2048)])
+def test_rmsnorm_chained_dw(monkeypatch, rows, cols):
     """Three stacked norms accumulating into persistent bf16 .grad (dw_mode 1): the first two weight gradients
     are reduced inside the NEXT norm's backward launch, the last by the end-of-backward callback
     (pico_rmsnorm_bwd_chain / pico_rmsnorm_dw_reduce). Same values as the one-launch-per-reduction path (same
     partial rows, fixed-order sums: within one bf16 rounding) and as the fp64 restatement, over two backward
-    passes (the second accumulates into the first's .grad)."""
+    passes (the second accumulates into the first's .grad). 5000 rows: the full 256-workgroup grid, two
+    passes of the row loop with a ragged second pass (some waves own one row, some none)."""
     ops = _ops()
     torch.manual_seed(cols)
-    rows = 512
     x0 = torch.randn(rows, cols, dtype=BF, device=DEV) * 2
     ws = [(1 + 0.1 * torch.randn(cols, device=DEV)).to(BF) for _ in range(3)]
     dys = [torch.randn(rows, cols, dtype=BF, device=DEV) for _ in range(2)]
