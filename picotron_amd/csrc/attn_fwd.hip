@@ -503,6 +503,18 @@ int launch_fwd(const pico_attn_args* a, hipStream_t s) {
 }  // namespace
 
 int pico_attn_check_common(const pico_attn_args* a, const char* op);
+bool pico_attn_fwd64_pp_ok(const pico_attn_args* a);         // attn_fwd64.hip
+int pico_attn_fwd64_pp(const pico_attn_args* a, hipStream_t s);
+
+// D = 64: the ping-pong kernel (attn_fwd64.hip) when PICO_ATTN_FWD64=1 (A/B against this file's 128-row
+// kernel; not the default until it is faster in the training step)
+static bool use_fwd64() {
+  static const int on = [] {
+    const char* e = getenv("PICO_ATTN_FWD64");
+    return e && e[0] == '1' ? 1 : 0;
+  }();
+  return on != 0;
+}
 
 extern "C" int pico_attn_fwd(const pico_attn_args* a, void* stream) {
   int rc = pico_attn_check_common(a, "pico_attn_fwd");
@@ -520,6 +532,9 @@ extern "C" int pico_attn_fwd(const pico_attn_args* a, void* stream) {
   }
   if (a->batch == 0 || a->seqlen_q == 0 || a->heads_q == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
-  if (a->head_dim == 64) return launch_fwd<64>(a, s);
+  if (a->head_dim == 64) {
+    if (use_fwd64() && pico_attn_fwd64_pp_ok(a)) return pico_attn_fwd64_pp(a, s);
+    return launch_fwd<64>(a, s);
+  }
   return launch_fwd<128>(a, s);
 }
