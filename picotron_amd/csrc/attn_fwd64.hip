@@ -59,9 +59,19 @@
 // k-slots of lanes 0-15 / 32-47 (query n) and 16-31 / 48-63 (query n + 16), so D[0][n] and D[1][n] are the
 // two queries' partial sums (of the bf16-rounded P the PV product uses): 4 MFMAs of 16 cycles per
 // segment instead of 36 VALU adds.
+// PICO_FWD64_QSCALE: S arrives from the matrix pipe already in the exp2 argument's units, so the softmax
+// needs no fma per score: q is prescaled by softmax_scale * log2(e) once (one extra bf16 rounding of q,
+// relative 2^-9 per element, below the bf16 rounding of P itself), and the running max enters the S chain
+// as one more MFMA, [ones | 0] x [-m | 0]^T (k-slot 0), so S' = scale log2e q.k - m. m is kept
+// bf16-representable (it is only a stabiliser); a rescale subtracts the change from the pending S' too.
+// Off: measured to break the LSE tolerance (C2: LSE max |err| 6.6e-3 vs 2e-3, O rel-L2 2.0e-3 -> 2.6e-3).
+#ifndef PICO_FWD64_QSCALE
+#define PICO_FWD64_QSCALE 0
+#endif
 #ifndef PICO_FWD64_LSUM
 #define PICO_FWD64_LSUM 1
 #endif
+static_assert(!PICO_FWD64_QSCALE || (PICO_FWD64_LSUM && PICO_FWD64_SCHED == 2), "QSCALE keeps l in the row-sum MFMA accumulator and needs the hand-ordered block");
 #ifndef PICO_FWD64_RD
 #define PICO_FWD64_RD 3  // operand reads issued this many MFMA slots ahead of their consumer
 #endif
@@ -77,6 +87,8 @@ constexpr int fwd64_chunk_op(int j, int c) {
                        f + 6, f + 7, v + 0, v + 1, e + 4, e + 5, e + 6, e + 7, v + 2, v + 3};
   return seq[j] + 10 * c;
 }
+// With S' prescaled (PICO_FWD64_QSCALE) a chunk is 8 exp2 then 4 cvt_pk (12 ops; C0 .. C3, 48 ops).
+constexpr int fwd64_op_qs(int k) { return (k % 12 < 8 ? 100 + k % 12 : 200 + k % 12 - 8) + 10 * (k / 12); }
 // With the row sums on the matrix pipe (PICO_FWD64_LSUM) the stream is C0 C1 C2 C3 only (80 ops).
 constexpr int fwd64_op_lsum(int k) { return fwd64_chunk_op(k % 20, k / 20); }
 constexpr int fwd64_op(int k) {
@@ -248,6 +260,26 @@ void attn_fwd64_kernel(const pico_attn_args a, float scale_log2, int round_len) 
         qf[x][ks + KS / 2] = __builtin_bit_cast(bf16x8, o2);
       }
   }
+  // With QSCALE the rotated rows leave now (the scaled copy replaces them in registers): 8 stores per lane,
+  // unconditional (rows past Sq rewrite row Sq - 1 with its own value), counted in the loop's first waits.
+  const int nq_st = (PICO_FWD64_QSCALE && rope_q) ? 2 * KS : 0;
+  if (PICO_FWD64_QSCALE && rope_q) {
+#pragma unroll
+    for (int x = 0; x < 2; ++x) {
+      const int row = min(qw + 32 * x + r, Sq - 1);
+      bf16_t* rq = (bf16_t*)a.dq + b * a.dq_strides[0] + hq * a.dq_strides[2] + (int64_t)row * a.dq_strides[1] + 8 * h;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) *reinterpret_cast<u16x8*>(rq + 16 * ks) = __builtin_bit_cast(u16x8, qf[x][ks]);
+    }
+  }
+  if (PICO_FWD64_QSCALE) {
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) qf[x][ks][j] = (__bf16)((float)qf[x][ks][j] * scale_log2);
+  }
 
   // ---- per-half causal / ragged limits (wave-uniform except lim_lane) ----
   int lim_first[2], last_t[2], lim_lane[2];
@@ -285,6 +317,14 @@ void attn_fwd64_kernel(const pico_attn_args a, float scale_log2, int round_len) 
     for (int j = 0; j < 8; ++j) ones_a[j] = (__bf16)(one ? 1.f : 0.f);
   }
   f32x4 ls16[2] = {(f32x4)0.f, (f32x4)0.f};
+  // PICO_FWD64_QSCALE: A = [1 | 0] (k-slot 0 of every key row: lanes h = 0, element 0) and per half
+  // B = [-m | 0] (k-slot 0 of query r: lane r, element 0), so mfma(ones_k, bias[x]) = -m broadcast
+  bf16x8 ones_k, bias[2];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    ones_k[j] = (__bf16)(j == 0 && h == 0 ? 1.f : 0.f);
+    bias[0][j] = bias[1][j] = (__bf16)0.f;
+  }
 
   // ---- building blocks ----
   // V^T operand for keys 32 kt + 16 st .. +15 of the tile, d tile dt (two ds_read_b64_tr_b16)
@@ -317,9 +357,26 @@ void attn_fwd64_kernel(const pico_attn_args a, float scale_log2, int round_len) 
       m0 = __builtin_fmaxf(m0, __builtin_fmaxf(S[x][0][i], S[x][0][i + 1]));
       m1 = __builtin_fmaxf(m1, __builtin_fmaxf(S[x][1][i], S[x][1][i + 1]));
     }
-    mt[x] = halves_max64(fmaxf(m0, m1)) * scale_log2;
+    mt[x] = halves_max64(fmaxf(m0, m1)) * (PICO_FWD64_QSCALE ? 1.f : scale_log2);
   };
   auto rescale = [&](int x) __attribute__((always_inline)) {
+#if PICO_FWD64_QSCALE
+    // mt[x] is the excess of the pending S' over the current m (m = -inf: none yet, bias 0, mt = the max)
+    if (__builtin_expect(__builtin_amdgcn_ballot_w64(mt[x] > (float)PICO_FWD64_THR || m[x] == -INFINITY) != 0, 0)) {
+      const bool first = m[x] == -INFINITY;
+      const float m_new = (float)(__bf16)((first ? 0.f : m[x]) + fmaxf(mt[x], first ? mt[x] : 0.f));
+      const float d = first ? m_new : m_new - m[x];  // exact: both bf16 values
+      const float alpha = first ? 0.f : fast_exp2(-d);
+      ls16[x][0] *= alpha;
+      ls16[x][1] *= __shfl(alpha, (lane & 15) + 16);
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) O[x][dt] *= alpha;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) S[x][kt] -= d;  // the pending S' was taken against the old m
+      m[x] = m_new;
+      bias[x][0] = (__bf16)(-m_new);
+    }
+#else
     if (__builtin_expect(__builtin_amdgcn_ballot_w64(mt[x] > m[x] + (float)PICO_FWD64_THR) != 0, 0)) {
       const float m_new = fmaxf(m[x], mt[x]);
       const float alpha = m[x] == -INFINITY ? 0.f : fast_exp2(m[x] - m_new);
@@ -332,6 +389,7 @@ void attn_fwd64_kernel(const pico_attn_args a, float scale_log2, int round_len) 
       for (int dt = 0; dt < DT; ++dt) O[x][dt] *= alpha;
       m[x] = m_new;
     }
+#endif
   };
   // P = exp2(scale log2e S - m) per 8-key step, packed to bf16 and fed at once to O^T += V^T P^T
   auto exp_pv = [&](int x, const char* vb) __attribute__((always_inline)) {
@@ -358,7 +416,7 @@ void attn_fwd64_kernel(const pico_attn_args a, float scale_log2, int round_len) 
   auto s_mfma = [&](int y, const char* kb) __attribute__((always_inline)) {
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
-      S[y][kt] = (f32x16)0.f;
+      S[y][kt] = PICO_FWD64_QSCALE ? mfma32(ones_k, bias[y], (f32x16)0.f) : (f32x16)0.f;
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) S[y][kt] = mfma32(lds_read_b128(kb, ks * KIMG + kt * 32 * 32), qf[y][ks], S[y][kt]);
     }
@@ -402,19 +460,22 @@ void attn_fwd64_kernel(const pico_attn_args a, float scale_log2, int round_len) 
           else mm = __builtin_fmaxf(mm, __builtin_fmaxf(S[Y][kt][2 * j], S[Y][kt][2 * j + 1]));
         });
       } else if constexpr (FOLD && i == 13) {
-        mt[Y] = halves_max64(fmaxf(m0, m1)) * scale_log2;
+        mt[Y] = halves_max64(fmaxf(m0, m1)) * (PICO_FWD64_QSCALE ? 1.f : scale_log2);
       }
     };
     const float neg_m = m[X] == -INFINITY ? 0.f : -m[X];
+    (void)neg_m;
     float ta[32], e[32], ls[4] = {0.f, 0.f, 0.f, 0.f};
     unsigned pk[16];
     auto valu = [&](auto k_tag) __attribute__((always_inline)) {
-      constexpr int op = PICO_FWD64_LSUM ? fwd64_op_lsum(decltype(k_tag)::value) : fwd64_op(decltype(k_tag)::value);
+      constexpr int op = PICO_FWD64_QSCALE ? fwd64_op_qs(decltype(k_tag)::value)
+                         : PICO_FWD64_LSUM ? fwd64_op_lsum(decltype(k_tag)::value) : fwd64_op(decltype(k_tag)::value);
       constexpr int ty = op / 100, c = (op / 10) % 10, j = op % 10, kt = c >> 1, st = c & 1;
       if constexpr (ty == 0) {
         ta[8 * c + j] = __builtin_fmaf(S[X][kt][8 * st + j], scale_log2, neg_m);
       } else if constexpr (ty == 1) {
-        e[8 * c + j] = (PICO_FWD64_ABL & 1) ? ta[8 * c + j] : fast_exp2(ta[8 * c + j]);
+        const float arg = PICO_FWD64_QSCALE ? S[X][kt][8 * st + j] : ta[8 * c + j];
+        e[8 * c + j] = (PICO_FWD64_ABL & 1) ? arg : fast_exp2(arg);
       } else if constexpr (ty == 2) {
         typedef __attribute__((ext_vector_type(2))) float f32x2;
         typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
@@ -430,7 +491,8 @@ void attn_fwd64_kernel(const pico_attn_args a, float scale_log2, int round_len) 
         else O[X][i & 1][0] += __builtin_bit_cast(float, pk[(i - 8) >> 1 << 2] ^ __builtin_bit_cast(unsigned, vf[i - 8][2] == vf[i-8][3] ? 1.f : 0.f));
       } else if constexpr (i < 8) {
         constexpr int kt = i >> 2, ks = i & 3;
-        S[Y][kt] = mfma32(kf[i], qf[Y][ks], ks == 0 ? (f32x16)0.f : S[Y][kt]);
+        if constexpr (ks == 0 && PICO_FWD64_QSCALE) S[Y][kt] = mfma32(ones_k, bias[Y], (f32x16)0.f);
+        S[Y][kt] = mfma32(kf[i], qf[Y][ks], (ks == 0 && !PICO_FWD64_QSCALE) ? (f32x16)0.f : S[Y][kt]);
       } else {
         constexpr int pp = i - 8, c = pp >> 1, dt = pp & 1;
         typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
@@ -441,8 +503,10 @@ void attn_fwd64_kernel(const pico_attn_args a, float scale_log2, int round_len) 
     };
     // VALU ops per slot: 7 each (112 ops), or with the MFMA row sums 6 each in slots 0-12 and 2 in slot 13
     // (80 ops; chunk c's last cvt_pk lands by slot 7 + 2c, before its PV MFMAs at slot 8 + 2c)
-    constexpr int NV = PICO_FWD64_LSUM ? 80 : 112;
-    auto ops_begin = [](int i) constexpr { return PICO_FWD64_LSUM ? (i * 6 < 80 ? i * 6 : 80) : 7 * i; };
+    constexpr int NV = PICO_FWD64_QSCALE ? 48 : PICO_FWD64_LSUM ? 80 : 112;
+    auto ops_begin = [](int i) constexpr {
+      return PICO_FWD64_QSCALE ? (i * 4 < 48 ? i * 4 : 48) : PICO_FWD64_LSUM ? (i * 6 < 80 ? i * 6 : 80) : 7 * i;
+    };
     __builtin_amdgcn_sched_barrier(0);
     static_for<16>([&](auto i_) {
       constexpr int i = decltype(i_)::value;
@@ -490,7 +554,8 @@ void attn_fwd64_kernel(const pico_attn_args a, float scale_log2, int round_len) 
   // is past segment B(t - 1), the last reader of tile t - 1's slot, which now takes tile t + 3
   auto barrier_dma = [&](int t) __attribute__((always_inline)) {
     if (!(PICO_FWD64_ABL & 4)) {
-      if (t + 1 < ntiles) wait_vmcnt(t + 2 < ntiles ? NIW : 0);
+      // younger than tile t + 1: tile t + 2 (if issued) and, for t + 1 <= NBUF - 2, the prologue's q stores
+      if (t + 1 < ntiles) wait_vmcnt((t + 2 < ntiles ? NIW : 0) + (t + 1 <= NBUF - 2 ? nq_st : 0));
       lds_barrier();
     }
     FWD64_ACC(3, tst);
@@ -545,7 +610,7 @@ void attn_fwd64_kernel(const pico_attn_args a, float scale_log2, int round_len) 
     const bool row_ok = my_q < Sq;
     bf16_t* op = (bf16_t*)a.o + b * a.o_strides[0] + hq * a.o_strides[2] + (int64_t)min(my_q, Sq - 1) * a.o_strides[1];
     store_row_bf16_x16<DT>(op, h, row_ok, [&](int dt, int i) { return O[x][dt][i] * inv[x]; });
-    if (rope_q && row_ok) {
+    if (!PICO_FWD64_QSCALE && rope_q && row_ok) {
       bf16_t* rq = (bf16_t*)a.dq + b * a.dq_strides[0] + hq * a.dq_strides[2] + (int64_t)my_q * a.dq_strides[1] + 8 * h;
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) *reinterpret_cast<u16x8*>(rq + 16 * ks) = __builtin_bit_cast(u16x8, qf[x][ks]);
