@@ -31,6 +31,7 @@ FILE_FLAGS = {
     "attn_fwd.hip": ["-fno-slp-vectorize"],
     "attn_fwd64.hip": ["-fno-slp-vectorize", "-fno-honor-nans", "-mllvm", "-amdgpu-mfma-vgpr-form"],
     "attn_bwd_split_d128.hip": ["-fno-slp-vectorize"],
+    "attn_bwd_q64.hip": ["-fno-slp-vectorize", "-mllvm", "-amdgpu-mfma-vgpr-form"],
 }
 
 

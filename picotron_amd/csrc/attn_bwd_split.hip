@@ -1041,6 +1041,26 @@ int kv_front(const pico_attn_args* a, int hsplit) {
   return first < nkb ? (int)(nkb - first) : 0;
 }
 
+}  // namespace
+bool pico_attn_bwd_q64_ok(const pico_attn_args* a);  // attn_bwd_q64.hip
+int pico_attn_bwd_q64(const pico_attn_args* a, hipStream_t s, float* lse2, float* delta, int sq_pad, int nfront);
+namespace {
+// D = 64 dQ: the tile-pipelined kernel (attn_bwd_q64.hip) when PICO_ATTN_BWDQ64=1 (A/B against attn_bwd_q_kernel)
+bool use_bwdq64() {
+  static const int on = [] {
+    const char* e = getenv("PICO_ATTN_BWDQ64");
+    return e && e[0] == '1' ? 1 : 0;
+  }();
+  return on != 0;
+}
+int q_front_minb(const pico_attn_args* a, int minb) {
+  if (!a->causal) return 0;
+  const int nmb = (int)((a->seqlen_q + QB - 1) / QB);
+  const int64_t nbh = a->batch * a->heads_q;
+  const int64_t first = (int64_t)pico_num_cus() * minb / (nbh > 0 ? nbh : 1);
+  return first < nmb ? (int)(nmb - first) : 0;
+}
+
 template <int D, bool CAUSAL>
 int launch_split(const pico_attn_args* a, hipStream_t s) {
   const int sq_pad = split_sq_pad(a);
@@ -1051,9 +1071,13 @@ int launch_split(const pico_attn_args* a, hipStream_t s) {
   const int nmb = (int)((a->seqlen_q + QB - 1) / QB);
   const int64_t gq = (int64_t)nmb * a->batch * a->heads_q;
   PICO_REQUIRE(gq < (1ll << 31), "pico_attn_bwd: grid too large");
-  PICO_TRY(pico_launch(PICO_K_ATTN_BWD_Q, "attn_bwd_q", attn_bwd_q_kernel<D, CAUSAL>, dim3((int)gq), dim3(256), 0, s, *a, a->softmax_scale, sl2, lse2, delta, sq_pad,
-                  (unsigned long long*)((char*)a->workspace + pico_attn_bwd_split_workspace(a) - STAMP_BYTES),
-                  q_front(a)));
+  if (D == 64 && use_bwdq64() && pico_attn_bwd_q64_ok(a)) {
+    PICO_TRY(pico_attn_bwd_q64(a, s, lse2, delta, sq_pad, q_front_minb(a, 2)));
+  } else {
+    PICO_TRY(pico_launch(PICO_K_ATTN_BWD_Q, "attn_bwd_q", attn_bwd_q_kernel<D, CAUSAL>, dim3((int)gq), dim3(256), 0, s, *a, a->softmax_scale, sl2, lse2, delta, sq_pad,
+                    (unsigned long long*)((char*)a->workspace + pico_attn_bwd_split_workspace(a) - STAMP_BYTES),
+                    q_front(a)));
+  }
   const int nkb = (int)((a->seqlen_k + KVB - 1) / KVB);
   const int hsplit = kv_hsplit(a);
   const int64_t nblk = (int64_t)nkb * a->batch * a->heads_kv * hsplit;
