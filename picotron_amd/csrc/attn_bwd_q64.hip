@@ -18,7 +18,7 @@
 #include "attn_common.h"
 
 // PICO_BQ64_ABL: ablation builds for timing only (results wrong): 1 no operand LDS reads, 2 no softmax VALU,
-// 4 no tile wait / barrier, 8 no M1 MFMAs, 16 no dQ MFMAs
+// 4 no tile wait / barrier, 8 no M1 MFMAs, 16 no dQ MFMAs, 32 no DMA in the loop (stale tiles)
 #ifndef PICO_BQ64_ABL
 #define PICO_BQ64_ABL 0
 #endif
@@ -305,7 +305,7 @@ void attn_bwd_q64_kernel(const pico_attn_args a, float scale, float scale_log2, 
       if (t + 1 < ntiles) wait_vmcnt(t + 2 < ntiles ? NPW : 0);
       lds_barrier();
     }
-    if (t + NBUF - 1 < ntiles) issue(t + NBUF - 1);
+    if (!(PICO_BQ64_ABL & 32) && t + NBUF - 1 < ntiles) issue(t + NBUF - 1);
   };
 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // prologue tiles and loads landed

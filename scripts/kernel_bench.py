@@ -73,6 +73,7 @@ def main(iters=50):
         ("rmsnorm_t", run_norm_t, [L.K_RMSNORM_FWD]),
         ("rmsnorm_chain", run_norm_chain, [L.K_RMSNORM_BWD]),
         ("rope", lambda: ops._rope_launch(qkv[:, :, :2 * NH], qkv[:, :, :2 * NH], cos, sin, False), [L.K_ROPE]),
+        ("rope_k", lambda: ops._rope_launch(qkv[:, :, NH:2 * NH], qkv[:, :, NH:2 * NH], cos, sin, False), [L.K_ROPE]),
         ("swiglu", lambda: (ops._swiglu_fwd(gu, gu[:, I:], h, T, I, 2 * I, I),
                             ops._swiglu_bwd(dh, gu, gu[:, I:], dgu, dgu[:, I:], T, I, 2 * I, I)),
          [L.K_SWIGLU_FWD, L.K_SWIGLU_BWD]),
@@ -92,6 +93,7 @@ def main(iters=50):
         if L.K_TRANSPOSE in kids:
             work[L.K_TRANSPOSE] = tbytes[name]
         work[L.K_SWIGLU_FWD] = (4 if name == "swiglu_t" else 3) * T * I * 2
+        work[L.K_ROPE] = 2 * T * (1 if name == "rope_k" else 2) * NH * D * 2
         for _ in range(3):
             fn()
         torch.cuda.synchronize()
@@ -103,7 +105,7 @@ def main(iters=50):
         for k in kids:
             ms, n = L.prof_collect(k)
             us = 1e3 * ms / max(n, 1)
-            out = {"kernel": L.KERNEL_NAMES[k] + ("" if k not in (L.K_TRANSPOSE,) and name not in ("rmsnorm_t", "swiglu_t", "rmsnorm_chain") else ":" + name), "avg_us": round(us, 2), "launches": n}
+            out = {"kernel": L.KERNEL_NAMES[k] + ("" if k not in (L.K_TRANSPOSE,) and name not in ("rmsnorm_t", "swiglu_t", "rmsnorm_chain", "rope_k") else ":" + name), "avg_us": round(us, 2), "launches": n}
             if k in work:
                 out["GB_s"] = round(work[k] / (us * 1e-6) / 1e9, 1)
                 out["frac_of_8TBs"] = round(out["GB_s"] / 8000, 3)
