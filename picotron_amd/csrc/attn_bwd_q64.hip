@@ -18,7 +18,8 @@
 #include "attn_common.h"
 
 // PICO_BQ64_ABL: ablation builds for timing only (results wrong): 1 no operand LDS reads, 2 no softmax VALU,
-// 4 no tile wait / barrier, 8 no M1 MFMAs, 16 no dQ MFMAs, 32 no DMA in the loop (stale tiles)
+// 4 no tile wait / barrier, 8 no M1 MFMAs, 16 no dQ MFMAs, 32 no DMA in the loop (stale tiles), 64 the softmax VALU
+// without dependencies (same op counts, every op reads S / dP), 128 exp2 replaced by a plain multiply
 #ifndef PICO_BQ64_ABL
 #define PICO_BQ64_ABL 0
 #endif
@@ -280,8 +281,22 @@ void attn_bwd_q64_kernel(const pico_attn_args a, float scale, float scale_log2, 
       typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
       if constexpr ((PICO_BQ64_ABL & 2) != 0) {
         if constexpr (ty == 4) pk[4 * c + j] = __float_as_uint(sc[kt][8 * st + 2 * j]) ^ __float_as_uint(pc[kt][8 * st + 2 * j + 1]);
+      } else if constexpr ((PICO_BQ64_ABL & 64) != 0) {  // independent ops (each result consumed by an empty asm)
+        const float src = sc[kt][8 * st + (j & 7)], src2 = pc[kt][8 * st + (j & 7)];
+        float rr;
+        if constexpr (ty == 0) rr = __builtin_fmaf(src, scale_log2, nl2);
+        else if constexpr (ty == 1) rr = fast_exp2(src2);
+        else if constexpr (ty == 2) rr = src2 + ndl;
+        else if constexpr (ty == 3) rr = src * src2;
+        else {
+          typedef __attribute__((ext_vector_type(2))) float f32x2;
+          typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+          pk[4 * c + j] = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){src, src2}, bf16x2));
+          rr = 0.f;
+        }
+        asm volatile("" ::"v"(rr));
       } else if constexpr (ty == 0) ta[q] = __builtin_fmaf(sc[kt][8 * st + j], scale_log2, nl2);
-      else if constexpr (ty == 1) e[q] = fast_exp2(ta[q]);
+      else if constexpr (ty == 1) e[q] = (PICO_BQ64_ABL & 128) ? ta[q] * 1.0001f : fast_exp2(ta[q]);
       else if constexpr (ty == 2) d[q] = pc[kt][8 * st + j] + ndl;
       else if constexpr (ty == 3) ds[q] = e[q] * d[q];
       else pk[4 * c + j] = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){ds[8 * c + 2 * j], ds[8 * c + 2 * j + 1]}, bf16x2));
