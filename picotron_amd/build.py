@@ -9,6 +9,7 @@ Usage: python -m picotron_amd.build [--verbose] [--resource-usage]
 import argparse
 import concurrent.futures as cf
 import os
+import re
 import subprocess
 import sys
 
@@ -42,6 +43,8 @@ def sources():
 def _compile(src, extra, verbose):
     obj = os.path.join(OBJ, os.path.basename(src)[:-4] + ".o")
     deps = [src] + [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
+    with open(src) as f:  # a translation unit that #includes another .hip source (attn_bwd_split_d128.hip)
+        deps += [os.path.join(CSRC, m.group(1)) for m in re.finditer(r'#include "([^"]+\.hip)"', f.read())]
     deps.append(os.path.join(HERE, "..", "include", "picotron_hip.h"))
     if os.path.exists(obj) and not extra and all(os.path.getmtime(obj) >= os.path.getmtime(d) for d in deps):
         return obj, ""
