@@ -93,6 +93,12 @@ constexpr int64_t STAMP_BYTES = PICO_BWDKV_STAMP ? 8 * STAMP_T * STAMP_P * 8
 #ifndef PICO_BWDQ_MINB
 #define PICO_BWDQ_MINB 3  // dQ kernel workgroups per CU the register budget is sized for (168 VGPRs)
 #endif
+#ifndef PICO_BWDQ_NBUF128
+#define PICO_BWDQ_NBUF128 2  // 64 KiB: two workgroups per CU (C4 dQ 36.5 -> 33.8 us, GQA-4 44.5 -> 39.4)
+#endif
+#ifndef PICO_BWDQ_MINB128
+#define PICO_BWDQ_MINB128 2  // the same for head_dim 128 (248 VGPRs with V read after the S chain)
+#endif
 #ifndef PICO_BWDQ_SPLITKT
 #define PICO_BWDQ_SPLITKT 1  // A/B C2 (us): 45.7 -> 44.1 with MINB 3; S 4096: 115.9 -> 107.4
 #endif
@@ -102,10 +108,10 @@ struct QCfg {
   static constexpr int KS = D / 16, DT = D / 32, CPR = D / 8, RB = 2 * D;
   // workgroups per CU the register budget is sized for: D = 128 holds 2x the fragments and dQ accumulators
   // (≈ 290 registers with the AGPRs its own translation unit may use: one workgroup per CU)
-  static constexpr int MINB = D == 64 ? PICO_BWDQ_MINB : 1;
+  static constexpr int MINB = D == 64 ? PICO_BWDQ_MINB : PICO_BWDQ_MINB128;
   static constexpr int IMG = KT * RB;          // one K (or V) tile image (lds_off<D> layout)
   static constexpr int SLOT = 2 * IMG;         // K | V
-  static constexpr int NBUF = PICO_BWDQ_NBUF;  // ring slots; prefetch distance NBUF - 1
+  static constexpr int NBUF = D == 64 ? PICO_BWDQ_NBUF : PICO_BWDQ_NBUF128;  // ring slots; prefetch NBUF - 1
   static constexpr int RPP = 1024 / RB;        // image rows per 1-KiB DMA piece
   static constexpr int NP = SLOT / 1024;       // pieces per tile
   static constexpr int NPW = NP / 4;           // per wave
@@ -302,11 +308,14 @@ __global__ __launch_bounds__(256, QCfg<D>::MINB) void attn_bwd_q_kernel(const pi
     const char* vb = kb + C::IMG;
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
+      // D = 128 at two workgroups per CU (PICO_BWDQ_MINB128 = 2): V's fragments are read after the S chain has
+      // consumed K's (32 fewer live VGPRs)
+      constexpr bool seqv = D == 128 && PICO_BWDQ_MINB128 > 1;
       bf16x8 kf[KS], vf[KS];
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
         kf[ks] = lds_read_b128(kb, ro[ks] + kt * 32 * RB);
-        vf[ks] = lds_read_b128(vb, ro[ks] + kt * 32 * RB);
+        if (!seqv) vf[ks] = lds_read_b128(vb, ro[ks] + kt * 32 * RB);
       }
       f32x16 sc, dpc;
       if (mask) {
@@ -320,6 +329,11 @@ __global__ __launch_bounds__(256, QCfg<D>::MINB) void attn_bwd_q_kernel(const pi
       }
 #pragma unroll
       for (int ks = 1; ks < KS; ++ks) sc = mfma32(kf[ks], qf[ks], sc);
+      if constexpr (seqv) {
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) vf[ks] = lds_read_b128(vb, ro[ks] + kt * 32 * RB);
+      }
       dpc = mfma32(vf[0], df[0], ndelta);
 #pragma unroll
       for (int ks = 1; ks < KS; ++ks) dpc = mfma32(vf[ks], df[ks], dpc);
