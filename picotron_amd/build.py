@@ -29,7 +29,7 @@ CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno
 # (cdna_hip_programming.md / MI355X_MICROARCH.md: packed f32 ops are an anti-lever there)
 FILE_FLAGS = {
     "attn_bwd_split.hip": ["-fno-slp-vectorize", "-mllvm", "-amdgpu-mfma-vgpr-form"],
-    "attn_fwd.hip": ["-fno-slp-vectorize"],
+    "attn_fwd.hip": ["-fno-slp-vectorize", "-fno-honor-nans"],
     "attn_fwd64.hip": ["-fno-slp-vectorize", "-fno-honor-nans", "-mllvm", "-amdgpu-mfma-vgpr-form"],
     "attn_bwd_split_d128.hip": ["-fno-slp-vectorize"],
     "attn_bwd_q64.hip": ["-fno-slp-vectorize", "-mllvm", "-amdgpu-mfma-vgpr-form"],
@@ -46,6 +46,7 @@ def _compile(src, extra, verbose):
     with open(src) as f:  # a translation unit that #includes another .hip source (attn_bwd_split_d128.hip)
         deps += [os.path.join(CSRC, m.group(1)) for m in re.finditer(r'#include "([^"]+\.hip)"', f.read())]
     deps.append(os.path.join(HERE, "..", "include", "picotron_hip.h"))
+    deps.append(os.path.abspath(__file__))  # per-file flags live here
     if os.path.exists(obj) and not extra and all(os.path.getmtime(obj) >= os.path.getmtime(d) for d in deps):
         return obj, ""
     cmd = [HIPCC, *CFLAGS, *FILE_FLAGS.get(os.path.basename(src), []), *extra, "-c", src, "-o", obj]
