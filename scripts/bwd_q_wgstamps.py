@@ -17,7 +17,7 @@ from picotron_amd import ops  # noqa: E402
 
 
 def main():
-    B, S, H, D = 4, 1024, 32, 64
+    B, S, H, D = (int(x) for x in os.environ.get("PICO_TL_SHAPE", "4,1024,32,64").split(","))  # C4: 2,1024,16,128
     torch.manual_seed(0)
     q, k, v, do = [torch.randn(B, S, H, D, device="cuda", dtype=torch.bfloat16) for _ in range(4)]
     o, lse = ops.attention_block_fwd(q, k, v, 1 / math.sqrt(D), True)
