@@ -66,6 +66,10 @@ def main():
             # MFMA busy cycles summed over SIMDs vs available SIMD-cycles (1024 SIMDs x GUI cycles / 8 XCD sum)
             simd_cycles = 1024 * cs["GRBM_GUI_ACTIVE"] / 8
             print(f"   MFMA busy fraction                      {cs['SQ_VALU_MFMA_BUSY_CYCLES'] / simd_cycles:8.3f}")
+        if "SQ_VALU_MFMA_BUSY_CYCLES" in cs:
+            # the same over the kernel's median duration at the 2.4 GHz MFMA clock (GRBM_GUI_ACTIVE can span more than
+            # the dispatch for short kernels: the effective clock above then reads high and the fraction low)
+            print(f"   MFMA busy fraction (median dur, 2.4 GHz) {cs['SQ_VALU_MFMA_BUSY_CYCLES'] / (1024 * ns * 2.4):8.3f}")
         if "SQ_LDS_BANK_CONFLICT" in cs and "SQ_LDS_IDX_ACTIVE" in cs:
             print(f"   LDS bank-conflict share                 {cs['SQ_LDS_BANK_CONFLICT'] / max(1, cs['SQ_LDS_IDX_ACTIVE']):8.3f}")
         if "FETCH_SIZE" in cs:
