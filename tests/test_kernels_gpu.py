@@ -844,3 +844,23 @@ def test_rmsnorm_fwd_transposed_output(rows, cols, res):
     if res:
         assert torch.equal(out[1], out_ref[1])
     assert torch.equal(y._pico_t, y.t())
+
+
+def test_attention_opt_in_kernels_parity():
+    """The opt-in D = 64 kernels (two-half forward PICO_ATTN_FWD64, tile-pipelined dQ PICO_ATTN_BWDQ64; read
+    once per process, so checked in one child process): scripts/attn_check.py's causal / ragged / odd /
+    non-causal cases against the fp32 reference, rel-L2 <= 1e-2 (its own gate; the shipped kernels measure
+    2.0-2.5e-3 there)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PICO_ATTN_FWD64="1", PICO_ATTN_BWDQ64="1")
+    r = subprocess.run([sys.executable, os.path.join(root, "scripts", "attn_check.py"), "--cases", "c2,odd,ragged,full"],
+                       env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    rows = [json.loads(line) for line in r.stdout.splitlines() if line.startswith("{")]
+    assert len(rows) == 4
+    for row in rows:
+        assert max(row["o"], row["dq"], row["dk"], row["dv"]) < 5e-3, row
