@@ -54,6 +54,11 @@
 #ifndef PICO_FWD_WGSTAMP
 #define PICO_FWD_WGSTAMP 0
 #endif
+// PICO_FWD_NOWAIT: ablation build (results wrong, timing only) -- the loop never waits for its K/V DMA: the
+// time the per-tile vmcnt waits cost
+#ifndef PICO_FWD_NOWAIT
+#define PICO_FWD_NOWAIT 0
+#endif
 
 // PICO_FWD_SNAKE: causal block order. The grid is dispatched in rounds of one workgroup per CU; when every
 // workgroup is resident at once (C2: 1024 = 4 per CU) each CU keeps the blocks one round hands it, so a
@@ -406,7 +411,8 @@ __attribute__((amdgpu_waves_per_eu(FwdCfg<D>::WAVES_PER_EU, FwdCfg<D>::WAVES_PER
 #endif
   for (int t = 0; t < ntiles; ++t) {
     // tile t's pieces landed (this wave's), then every wave's (barrier); later tiles stay in flight
-    if (P == 2 && t + 1 < ntiles) {
+    if (PICO_FWD_NOWAIT) {  // ablation (results wrong, timing only): no wait for the tile's DMA
+    } else if (P == 2 && t + 1 < ntiles) {
       if constexpr (C::NIW == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     } else {
