@@ -40,14 +40,20 @@ def sources():
     return sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".hip"))
 
 
+def deps(src):
+    """Files whose change rebuilds `src`: itself, every csrc header, the C-ABI header, this file (per-file
+    flags) and any .hip source it #includes (attn_bwd_split_d128.hip includes attn_bwd_split.hip)."""
+    out = [src] + [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
+    with open(src) as f:
+        out += [os.path.join(CSRC, m.group(1)) for m in re.finditer(r'#include "([^"]+\.hip)"', f.read())]
+    out.append(os.path.join(HERE, "..", "include", "picotron_hip.h"))
+    out.append(os.path.abspath(__file__))
+    return out
+
+
 def _compile(src, extra, verbose):
     obj = os.path.join(OBJ, os.path.basename(src)[:-4] + ".o")
-    deps = [src] + [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
-    with open(src) as f:  # a translation unit that #includes another .hip source (attn_bwd_split_d128.hip)
-        deps += [os.path.join(CSRC, m.group(1)) for m in re.finditer(r'#include "([^"]+\.hip)"', f.read())]
-    deps.append(os.path.join(HERE, "..", "include", "picotron_hip.h"))
-    deps.append(os.path.abspath(__file__))  # per-file flags live here
-    if os.path.exists(obj) and not extra and all(os.path.getmtime(obj) >= os.path.getmtime(d) for d in deps):
+    if os.path.exists(obj) and not extra and all(os.path.getmtime(obj) >= os.path.getmtime(d) for d in deps(src)):
         return obj, ""
     cmd = [HIPCC, *CFLAGS, *FILE_FLAGS.get(os.path.basename(src), []), *extra, "-c", src, "-o", obj]
     if verbose:

@@ -152,3 +152,14 @@ def test_weight_transpose_cache_host_logic(monkeypatch):
     gc.collect()
     ops._wt_purge()
     assert len(ops._WT_CACHE) == 0
+
+
+def test_build_tracks_included_sources():
+    """A translation unit that #includes another .hip source is rebuilt when that source changes (a stale
+    attn_bwd_split_d128.o once sized its dK/dV partial writes for another split count than the workspace)."""
+    import os
+    from picotron_amd import build as B
+    d128 = os.path.join(B.CSRC, "attn_bwd_split_d128.hip")
+    deps = B.deps(d128)
+    assert os.path.join(B.CSRC, "attn_bwd_split.hip") in deps
+    assert os.path.abspath(B.__file__) in deps
