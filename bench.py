@@ -8,8 +8,9 @@ reference README / config 3 per-GPU workload; weak scaling over DP), bf16, rando
 reference's init procedure, synthetic uniform tokens already resident on the GPU.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--grad-acc G] [--no-cpu-baseline]
-For N > 1 the driver launches one process per GPU with torch.distributed.run; DP gradients are
-all-reduced over RCCL (xGMI) by DataParallelBucket.
+For N > 1 the driver launches one process per GPU with torch.distributed.run (`python bench.py --gpus N`
+without that launcher starts it itself, before touching the GPU); DP gradients are all-reduced over RCCL
+(xGMI) by DataParallelBucket.
 
 Rank 0 prints ONE JSON line with `value` = whole-job tokens/s, a `roofline` object for the
 dominant kernel (timed live with HIP events on its own launch stream) and a `cpu_baseline` object
@@ -63,10 +64,9 @@ def kernel_work(kid, cfg, mbs, seq):
     Hkv = cfg.num_key_value_heads
     D = Hd // H
     attn_fwd = 4.0 * mbs * H * seq * seq * D / 2  # causal
-    nkb = -(-seq // 256)  # 256-key blocks of the backward
-    dq_slabs = sum(min(nkb, q // 256 + 1) for q in range(seq)) / seq  # causal: mean slabs per query row
     table = {
         L.K_ATTN_FWD: (attn_fwd, "flop", "mfma"),
+        # the backward as one operation (5 products): the roofline prices the dQ + dK/dV pair on it
         L.K_ATTN_BWD: (2.5 * attn_fwd, "flop", "mfma"),
         # split backward (head_dim 64, csrc/attn_bwd_split.hip): EXECUTED products per kernel — the dQ kernel
         # recomputes S and dP (3 products), the dK/dV kernel 4; the roofline entry for the backward prices
@@ -82,20 +82,56 @@ def kernel_work(kid, cfg, mbs, seq):
         L.K_ROPE: (2 * T * (Hkv + (H if os.getenv("PICO_FUSE_ROPE_Q", "1") == "0" else 0)) * D * 2, "byte", "hbm"),
         L.K_SWIGLU_FWD: (4 * T * I * 2, "byte", "hbm"),  # g, u read; h and h^T written
         L.K_SWIGLU_BWD: (5 * T * I * 2, "byte", "hbm"),
-        # reads O, dO, LSE; writes delta and LSE*log2(e) (fp32 per query row and head)
-        L.K_ATTN_BWD_PRE: (2 * T * Hd * 2 + 3 * T * H * 4, "byte", "hbm"),
-        # reads the fp32 dQ partial slabs of the key blocks at or before each query row, writes bf16 dQ;
-        # RoPE^-1 of dK in place in the same launch (read + write)
-        L.K_ATTN_BWD_DQ: (dq_slabs * T * Hd * 4 + T * Hd * 2 + 2 * T * Hkv * D * 2, "byte", "hbm"),
     }
     return table.get(kid)
 
 
+def _spawn_workers(n):
+    """`--gpus N` without a launcher: run this script under torch.distributed.run with N ranks (one per GPU) as a
+    child process and return its exit code. Called before this process touches the GPU; rank 0 of the child job
+    writes the JSON line to the stdout this process inherited."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n), "--master-addr",
+           "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *sys.argv[1:]]
+    log(f"[launcher] --gpus {n} without WORLD_SIZE: " + " ".join(cmd))
+    return subprocess.call(cmd, env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0"))
+
+
+def setup(layers, grad_acc, world, device, optimizer="pico", fused_adam=True, post_build=None):
+    """The benchmark's model, optimizer and data (also used by tests/test_dp_hip_gpu.py's C3 check, so both run
+    the same step): SmolLM-1.7B geometry with `layers` layers at seq 1024, the reference's random init with seed 42
+    on every rank (identical replicas, ref train.py:103), DataParallelBucket when world > 1 (the bf16 .grad cast
+    fused into the pico AdamW step), AdamW lr 3e-4 (ref train.py:204-209), synthetic uniform tokens resident on the
+    device. post_build(model) runs before the DP wrapper (tests: a non-zero LM head)."""
+    from picotron_amd.data import SyntheticDataLoader
+    from picotron_amd.data_parallel.data_parallel import DataParallelBucket
+    from picotron_amd.model import build_llama, smollm_1_7b
+    cfg = smollm_1_7b(num_hidden_layers=layers, seq_length=SEQ)
+    torch.manual_seed(42)  # ref train.py:103 (same seed on every rank: identical replicas)
+    model = build_llama(cfg, device=device, dtype=torch.bfloat16)
+    if post_build is not None:
+        post_build(model)
+    num_params = sum(p.numel() for p in model.parameters())
+    if world > 1:
+        # the bf16 .grad cast (ref data_parallel.py:165) fused into the pico AdamW step (bit-identical)
+        model = DataParallelBucket(model, defer_grad_cast=optimizer == "pico")
+    # ref train.py:204-209: AdamW(lr), fused when the config's use_fused_adam is set (template default true)
+    if optimizer == "pico":
+        from picotron_amd.optim import AdamW
+        opt = AdamW(model.parameters(), lr=3e-4)
+    else:
+        opt = torch.optim.AdamW(model.parameters(), lr=3e-4, **({"fused": True} if fused_adam else {}))
+    loader = SyntheticDataLoader(MBS, SEQ, grad_acc, cfg.vocab_size, seed=1234, kind="uniform",
+                                 num_batches=grad_acc, device=device)
+    return cfg, model, opt, loader, num_params
+
+
 def main():
-    # Keep stdout for the ONE JSON line: native libraries (RCCL prints a banner at communicator
-    # creation) write to fd 1, so point fd 1 at stderr and write the result to the saved fd.
-    json_fd = os.dup(1)
-    os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
@@ -119,12 +155,18 @@ def main():
     ap.add_argument("--graphs", type=int, default=1,
                     help="replay non-syncing micro-batches as a HIP graph (1) or run them eagerly (0)")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        raise SystemExit(_spawn_workers(args.gpus))
+    # Keep stdout for the ONE JSON line: native libraries (RCCL prints a banner at communicator
+    # creation) write to fd 1, so point fd 1 at stderr and write the result to the saved fd.
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     # CPU baseline first, before this process touches the GPU (its gloo ranks are fresh processes):
     # BASELINE.md's CPU plan, DP = 2 x 4 threads, SmolLM-1.7B geometry 2 layers, seq 1024 (oracle/cpu_baseline.py)
     cpu_baseline = None
@@ -151,56 +193,22 @@ def main():
 
     from picotron_amd import _lib as L
     from picotron_amd import process_group_manager as pgm
-    from picotron_amd.data import SyntheticDataLoader
-    from picotron_amd.data_parallel.data_parallel import DataParallelBucket
-    from picotron_amd.model import build_llama, smollm_1_7b
-    from picotron_amd.train import MicroBatchGraph, get_mfu, train_step
+    from picotron_amd.train import TrainingStep, get_mfu, train_step
 
     L.load()
     pgm.setup_process_group_manager(tp_size=1, cp_size=1, pp_size=1, dp_size=world)
-    cfg = smollm_1_7b(num_hidden_layers=args.layers, seq_length=SEQ)
-    torch.manual_seed(42)  # ref train.py:103 (same seed on every rank: identical replicas)
     t0 = time.time()
-    model = build_llama(cfg, device=device, dtype=torch.bfloat16)
-    num_params = sum(p.numel() for p in model.parameters())
-    if world > 1:
-        # the bf16 .grad cast (ref data_parallel.py:165) fused into the pico AdamW step (bit-identical)
-        model = DataParallelBucket(model, defer_grad_cast=args.optimizer == "pico")
-    # ref train.py:204-209: AdamW(lr), fused when the config's use_fused_adam is set (template default true)
-    if args.optimizer == "pico":
-        from picotron_amd.optim import AdamW
-        opt = AdamW(model.parameters(), lr=3e-4)
-    else:
-        opt = torch.optim.AdamW(model.parameters(), lr=3e-4, **({"fused": True} if args.fused_adam else {}))
-    loader = SyntheticDataLoader(MBS, SEQ, args.grad_acc, cfg.vocab_size, seed=1234, kind="uniform",
-                                 num_batches=args.grad_acc, device=device)
+    cfg, model, opt, loader, num_params = setup(args.layers, args.grad_acc, world, device, args.optimizer,
+                                                bool(args.fused_adam))
     log(f"[rank {rank}] model {num_params / 1e9:.3f}B params built in {time.time() - t0:.1f}s")
-
-    def zero_grads():
-        for p in model.parameters():
-            if p.grad is not None:
-                p.grad.zero_()
-        if hasattr(model, "bucket_manager"):
-            model.bucket_manager.reset()
-
-    graphs = MicroBatchGraph(model, args.grad_acc, zero_grads) if args.graphs else None
-
-    def step(sync=True):
-        # graphs: gradient buffers must persist (zeroed in place); eager: the reference's set_to_none
-        opt.zero_grad(set_to_none=graphs is None)
-        loss = train_step(model, loader, device, graphs=graphs, sync_loss=sync)
-        opt.step()
-        if hasattr(model, "reset"):
-            model.reset()
-        return loss
+    step = TrainingStep(model, opt, loader, device, graphs=bool(args.graphs))
 
     for i in range(args.warmup):
         ts = time.time()
         loss = step()
         log(f"[rank {rank}] warmup {i}: loss {loss:.4f} ({time.time() - ts:.2f}s)")
 
-    kernel_ids = [L.K_ATTN_FWD, L.K_ATTN_BWD, L.K_ATTN_BWD_Q, L.K_ATTN_BWD_KV, L.K_ATTN_BWD_PRE, L.K_ATTN_BWD_DQ,
-                  L.K_ATTN_BWD_DKV, L.K_RMSNORM_FWD, L.K_RMSNORM_BWD,
+    kernel_ids = [L.K_ATTN_FWD, L.K_ATTN_BWD_Q, L.K_ATTN_BWD_KV, L.K_ATTN_BWD_DKV, L.K_RMSNORM_FWD, L.K_RMSNORM_BWD,
                   L.K_RMSNORM_DW, L.K_ROPE, L.K_SWIGLU_FWD, L.K_SWIGLU_BWD, L.K_GRAD_ACCUM, L.K_CAST]
     # Per-launch HIP events cannot ride inside a graph replay, so with graphs the kernels are timed
     # over one extra eagerly launched step right after the timed region (same shapes, same stream).
@@ -217,7 +225,7 @@ def main():
     for i in range(args.steps):
         # the loss stays on the device until the timed region ends: no host sync inside it (the host queues
         # step i + 1 while the device runs step i; --sync-steps restores one .item() per step)
-        losses.append(step(sync=args.sync_steps))
+        losses.append(step(sync_loss=args.sync_steps))
     torch.cuda.synchronize()
     dist.barrier()
     elapsed = time.perf_counter() - t_start

@@ -57,7 +57,7 @@ enum {
   PICO_K_SWIGLU_FWD = 5,
   PICO_K_SWIGLU_BWD = 6,
   PICO_K_ATTN_FWD = 7,
-  PICO_K_ATTN_BWD_PRE = 8,
+  PICO_K_ATTN_BWD_PRE = 8, /* 8-10: retired with round 1's fused backward (kept so later ids stay stable) */
   PICO_K_ATTN_BWD = 9,
   PICO_K_ATTN_BWD_DQ = 10,
   PICO_K_GRAD_ACCUM = 11,
@@ -71,8 +71,8 @@ enum {
   PICO_K_ATTN_BWD_DKV = 19,
   PICO_K_SORT_IDS = 20,
   PICO_K_ADAMW = 21,
-  PICO_K_ATTN_BWD_KV = 22, /* split backward (D = 64): dK/dV key-major kernel */
-  PICO_K_ATTN_BWD_Q = 23,  /* split backward (D = 64): dQ query-major kernel (+ delta, LSE*log2e) */
+  PICO_K_ATTN_BWD_KV = 22, /* split backward: dK/dV key-major kernel */
+  PICO_K_ATTN_BWD_Q = 23,  /* split backward: dQ query-major kernel (+ delta, LSE*log2e) */
   PICO_K_COUNT = 24
 };
 

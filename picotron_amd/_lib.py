@@ -21,7 +21,7 @@ K_ATTN_BWD_KV, K_ATTN_BWD_Q = 22, 23
 KERNEL_NAMES = {
     K_RMSNORM_FWD: "rmsnorm_fwd", K_RMSNORM_BWD: "rmsnorm_bwd", K_RMSNORM_DW: "rmsnorm_dw", K_ROPE: "rope",
     K_SWIGLU_FWD: "swiglu_fwd", K_SWIGLU_BWD: "swiglu_bwd", K_ATTN_FWD: "attn_fwd",
-    K_ATTN_BWD_PRE: "attn_bwd_pre", K_ATTN_BWD: "attn_bwd", K_ATTN_BWD_DQ: "attn_bwd_dq",
+    K_ATTN_BWD_PRE: "retired_8", K_ATTN_BWD: "retired_9", K_ATTN_BWD_DQ: "retired_10",
     K_GRAD_ACCUM: "grad_accum", K_CAST: "cast_f32_bf16", K_SCALE: "scale_f32", K_ATTN_MERGE: "attn_merge",
     K_EMBEDDING_BWD: "embedding_bwd", K_CE_FWD: "cross_entropy_fwd", K_CE_BWD: "cross_entropy_bwd",
     K_TRANSPOSE: "transpose_bf16", K_ATTN_BWD_DKV: "attn_bwd_dkv", K_SORT_IDS: "sort_ids", K_ADAMW: "adamw",

@@ -30,9 +30,7 @@ CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno
 FILE_FLAGS = {
     "attn_bwd_split.hip": ["-fno-slp-vectorize", "-mllvm", "-amdgpu-mfma-vgpr-form"],
     "attn_fwd.hip": ["-fno-slp-vectorize", "-fno-honor-nans"],
-    "attn_fwd64.hip": ["-fno-slp-vectorize", "-fno-honor-nans", "-mllvm", "-amdgpu-mfma-vgpr-form"],
     "attn_bwd_split_d128.hip": ["-fno-slp-vectorize"],
-    "attn_bwd_q64.hip": ["-fno-slp-vectorize", "-mllvm", "-amdgpu-mfma-vgpr-form"],
 }
 
 

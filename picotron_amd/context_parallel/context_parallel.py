@@ -101,14 +101,23 @@ def _merge_bshd(out, lse, block_out, block_lse):
 
 
 def update_out_and_lse(out, lse, block_out, block_lse, slice_=None):
-    """ref :157-187, same signature and layout: block_out [B, H, S, D] (bf16 or fp32), block_lse [B, H, S];
-    the running out is fp32 [B, H, S, D] and lse fp32 [B, H, S, 1]. The first call (out None) returns
-    (block_out as fp32, block_lse[..., None]) as new tensors; later calls merge in place (the reference's
-    `_update` rebinds; its results are the same values) and return (out, lse). slice_ merges into
-    out[slice_] / lse[slice_] only (e.g. the rows of one query chunk), as the reference does; the first call
-    with a slice_ raises, as there. Runs on pico_attn_merge through element strides (no copies)."""
+    """ref :157-187, same signature, layout and semantics: block_out [B, H, S, D], block_lse [B, H, S]; the running
+    out is fp32 [B, H, S, D] and lse fp32 [B, H, S, 1].
+      * first call (out None): returns (block_out as fp32, block_lse[..., None]) as new tensors; with slice_ it
+        raises, as there;
+      * slice_ given: merges into out[slice_] / lse[slice_] IN PLACE (the reference's slice assignment) and returns
+        (out, lse);
+      * otherwise: returns NEW merged tensors and leaves the caller's out / lse untouched, as the reference's
+        `_update` rebinding does (one fp32 copy each; the ring itself merges in place through _merge_bshd).
+    Operands of other dtypes are cast as the reference does (block_out.to(fp32) when it is neither bf16 — read
+    natively by the kernel — nor fp32; block_lse and a non-slice running out / lse to fp32). Runs on
+    pico_attn_merge through element strides."""
     if block_out.dim() != 4 or block_lse.dim() != 3 or tuple(block_lse.shape) != tuple(block_out.shape[:3]):
         raise ValueError("update_out_and_lse: block_out must be [B, H, S, D] and block_lse [B, H, S]")
+    if block_out.dtype not in (torch.bfloat16, torch.float32):
+        block_out = block_out.to(torch.float32)
+    if block_lse.dtype != torch.float32:
+        block_lse = block_lse.to(torch.float32)
     if block_out.stride(-1) != 1:
         block_out = block_out.contiguous()
     B, H, S, D = block_out.shape
@@ -119,9 +128,16 @@ def update_out_and_lse(out, lse, block_out, block_lse, slice_=None):
         lse = torch.empty((B, H, S, 1), dtype=torch.float32, device=block_out.device)
         first = True
         ov, lv = out, lse
+    elif slice_ is not None:
+        first = False
+        if out.dtype != torch.float32 or lse.dtype != torch.float32:
+            raise TypeError("update_out_and_lse: an in-place (slice_) merge needs the fp32 running out / lse")
+        ov, lv = out[slice_], lse[slice_]
     else:
         first = False
-        ov, lv = (out[slice_], lse[slice_]) if slice_ is not None else (out, lse)
+        out = out.to(torch.float32, copy=True)
+        lse = lse.to(torch.float32, copy=True)
+        ov, lv = out, lse
     if ov.dim() != 4 or tuple(ov.shape) != (B, H, S, D) or ov.stride(-1) != 1 or \
             lv.dim() != 4 or tuple(lv.shape) != (B, H, S, 1):
         raise ValueError(f"update_out_and_lse: out{'[slice_]' if slice_ is not None else ''} must be [B, H, S, D] "

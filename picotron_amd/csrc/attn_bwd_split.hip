@@ -36,45 +36,16 @@ namespace {
 
 constexpr int QB = 128;  // dq kernel: query rows per workgroup (4 waves x 32)
 constexpr int KT = 64;   // dq kernel: keys per tile
-// dkv kernel workgroup: 128 keys = 4 waves (one per SIMD) of 32 keys, two workgroups resident per CU
-// (PICO_KV_MINB): independent workgroups overlap one's prologue (K/V fragments, first tiles) and epilogue
-// (dK/dV stores) with the other's main loop, which the 8-wave 256-key form (one workgroup per CU) could
-// not: C2 causal 62 vs 68 us.
-#ifndef PICO_KV_KVB
-#define PICO_KV_KVB 128
-#endif
-// Workgroups per CU the register budget is sized for (a template parameter, chosen per launch by kv_minb):
-// 3 (168 VGPRs) for causal grids, whose LPT-ordered uneven blocks fill any number of slots: C2 58.5 -> 52.6
-// us, S 4096 153 -> 143; 2 (256 VGPRs) for non-causal grids, whose equal blocks would leave a third round
-// partly empty (C2 full: 1024 blocks = 2 rounds of 512 slots vs 1.33 rounds of 768) and whose body spills
-// at 168 VGPRs (83 vs 123 us).
-#ifndef PICO_KV_MINB
-#define PICO_KV_MINB 0  // 0: per launch (kv_minb); 2 or 3: forced
-#endif
-constexpr int KVB = PICO_KV_KVB;  // dkv kernel: keys per workgroup
-// dkv kernel: keys per wave. 64: 4 waves, one per SIMD, 2 key halves each (each Q/dO tile read serves 64
-// keys); 32: 8 waves, two per SIMD (the partner wave covers one wave's DMA issue and MFMA -> VALU waits)
-#ifndef PICO_KV_KPW
-#define PICO_KV_KPW 32
-#endif
-constexpr int KPW = PICO_KV_KPW, KH = KPW / 32, KNW = KVB / KPW;
-constexpr int QT = 32;   // dkv kernel: query rows per tile
-#ifndef PICO_KV_SEQM1
-#define PICO_KV_SEQM1 1  // read dO's fragments after the S chain (-16 live VGPRs; C2 58.5 -> 56.1 us at MINB 2)
-#endif
-#ifndef PICO_KV_PIPE
-#define PICO_KV_PIPE 0
-#endif
-#ifndef PICO_KV_ROUND
-#define PICO_KV_ROUND 1
-#endif
+// dkv kernel workgroup: 128 keys = 4 waves (one per SIMD) of 32 keys. Two or three workgroups resident per CU
+// (kv_minb) overlap one's prologue (K/V fragments, first tiles) and epilogue (dK/dV stores) with the others' main
+// loops, which the 8-wave 256-key form (one workgroup per CU) could not: C2 causal 62 vs 68 us. Measured and
+// dropped: 64 keys per wave (69-71 vs 52 us), a tile-pipelined body carrying S / dP of tile
+// t + 1 across the barrier (+6 % at D = 64, noise at D = 128), two tiles per barrier interval.
+constexpr int KVB = 128;                  // dkv kernel: keys per workgroup
+constexpr int KPW = 32, KH = KPW / 32, KNW = KVB / KPW;  // keys per wave (one 32-key half), waves per workgroup
+constexpr int QT = 32;                    // dkv kernel: query rows per tile
 
-// PICO_BWDKV_STAMP: diagnostic build — workgroup 0 of the dK/dV kernel records s_memtime per (wave, tile,
-// phase) and writes them after the workspace (pico_attn_bwd_split_workspace grows by STAMP_BYTES)
-#ifndef PICO_BWDKV_STAMP
-#define PICO_BWDKV_STAMP 0
-#endif
-constexpr int STAMP_T = 48, STAMP_P = 5;
+// Diagnostic builds (scripts/gpu_attn_timeline.sh; results unchanged):
 // PICO_BWDKV_WGSTAMP: diagnostic build — every dK/dV workgroup records s_memrealtime (100 MHz, chip-wide)
 // at entry, loop start, loop end and after its stores drained (4 x 8 B per workgroup, grids <= 65536)
 #ifndef PICO_BWDKV_WGSTAMP
@@ -84,34 +55,19 @@ constexpr int STAMP_T = 48, STAMP_P = 5;
 #ifndef PICO_BWDQ_WGSTAMP
 #define PICO_BWDQ_WGSTAMP 0
 #endif
-constexpr int64_t STAMP_BYTES = PICO_BWDKV_STAMP ? 8 * STAMP_T * STAMP_P * 8
-                                                 : ((PICO_BWDKV_WGSTAMP || PICO_BWDQ_WGSTAMP) ? 65536 * 4 * 8 : 0);
+constexpr int64_t STAMP_BYTES = (PICO_BWDKV_WGSTAMP || PICO_BWDQ_WGSTAMP) ? 65536 * 4 * 8 : 0;
 
-#ifndef PICO_BWDQ_NBUF
-#define PICO_BWDQ_NBUF 3
-#endif
-#ifndef PICO_BWDQ_MINB
-#define PICO_BWDQ_MINB 3  // dQ kernel workgroups per CU the register budget is sized for (168 VGPRs)
-#endif
-#ifndef PICO_BWDQ_NBUF128
-#define PICO_BWDQ_NBUF128 2  // 64 KiB: two workgroups per CU (C4 dQ 36.5 -> 33.8 us, GQA-4 44.5 -> 39.4)
-#endif
-#ifndef PICO_BWDQ_MINB128
-#define PICO_BWDQ_MINB128 2  // the same for head_dim 128 (248 VGPRs with V read after the S chain)
-#endif
-#ifndef PICO_BWDQ_SPLITKT
-#define PICO_BWDQ_SPLITKT 1  // A/B C2 (us): 45.7 -> 44.1 with MINB 3; S 4096: 115.9 -> 107.4
-#endif
-
+// dQ kernel: ring slots and workgroups per CU the register budget is sized for. D = 64: 3 slots (48 KiB), three
+// workgroups per CU at 168 VGPRs (the two 32-key halves of a tile in turn: C2 45.7 -> 44.1 us, S 4096 115.9 ->
+// 107.4). D = 128: 2 slots (64 KiB), two workgroups per CU at 248 VGPRs (V's fragments read after the S chain):
+// C4 dQ 36.5 -> 33.8 us, GQA-4 44.5 -> 39.4.
 template <int D>
 struct QCfg {
   static constexpr int KS = D / 16, DT = D / 32, CPR = D / 8, RB = 2 * D;
-  // workgroups per CU the register budget is sized for: D = 128 holds 2x the fragments and dQ accumulators
-  // (≈ 290 registers with the AGPRs its own translation unit may use: one workgroup per CU)
-  static constexpr int MINB = D == 64 ? PICO_BWDQ_MINB : PICO_BWDQ_MINB128;
-  static constexpr int IMG = KT * RB;          // one K (or V) tile image (lds_off<D> layout)
-  static constexpr int SLOT = 2 * IMG;         // K | V
-  static constexpr int NBUF = D == 64 ? PICO_BWDQ_NBUF : PICO_BWDQ_NBUF128;  // ring slots; prefetch NBUF - 1
+  static constexpr int MINB = D == 64 ? 3 : 2;   // workgroups per CU (register budget 168 / 248 VGPRs)
+  static constexpr int IMG = KT * RB;            // one K (or V) tile image (lds_off<D> layout)
+  static constexpr int SLOT = 2 * IMG;           // K | V
+  static constexpr int NBUF = D == 64 ? 3 : 2;   // ring slots; prefetch NBUF - 1
   static constexpr int RPP = 1024 / RB;        // image rows per 1-KiB DMA piece
   static constexpr int NP = SLOT / 1024;       // pieces per tile
   static constexpr int NPW = NP / 4;           // per wave
@@ -123,11 +79,8 @@ struct KVCfg {
   static constexpr int QIMG = QT * RB;   // one Q (or dO) tile image
   static constexpr int LSD = 1024;       // LSE*log2e [32] | -delta [32] (one DMA piece)
   static constexpr int SLOT = 2 * QIMG + LSD;
-  // PICO_KV_ROUND: tiles per barrier interval (one wait + barrier + DMA issue serves R tiles);
-  // PICO_KV_PIPE: the interval of tile t also reads slot t + 1 (S / dP of the next tile), so one more slot
-  static constexpr int R = PICO_KV_PIPE ? 1 : PICO_KV_ROUND;
-  static constexpr int PD = PICO_KV_PIPE ? 3 : 2 * R;   // prefetch distance (tiles): two intervals ahead
-  static constexpr int NBUF = PICO_KV_PIPE ? 4 : 3 * R;  // ring slots
+  static constexpr int PD = 2;    // prefetch distance (tiles)
+  static constexpr int NBUF = 3;  // ring slots
   static constexpr int RPP = 1024 / RB;
   static constexpr int NQP = QIMG / 1024;
   static constexpr int NP = 2 * NQP + 1;
@@ -301,16 +254,15 @@ __global__ __launch_bounds__(256, QCfg<D>::MINB) void attn_bwd_q_kernel(const pi
   // One 64-key tile: S^T, dP^T (8 + 8 MFMAs), P^T and dS^T in registers, dQ^T += K^T dS^T (8 MFMAs).
   // kb: the slot's K image (V image at +IMG). One body for every tile (the causal / padding mask is an
   // in-place branch on S), so the loop-carried dQ accumulators never move between registers.
-#if PICO_BWDQ_SPLITKT
   // the two 32-key halves of a tile one after the other (half the K / V fragments and S / dP registers
-  // live at a time: room for a third workgroup per CU, PICO_BWDQ_MINB)
+  // live at a time: room for a third workgroup per CU at D = 64)
   auto tile = [&](const char* kb, bool mask, int n0) __attribute__((always_inline)) {
     const char* vb = kb + C::IMG;
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
-      // D = 128 at two workgroups per CU (PICO_BWDQ_MINB128 = 2): V's fragments are read after the S chain has
+      // D = 128 at two workgroups per CU (248 VGPRs): V's fragments are read after the S chain has
       // consumed K's (32 fewer live VGPRs)
-      constexpr bool seqv = D == 128 && PICO_BWDQ_MINB128 > 1;
+      constexpr bool seqv = D == 128;
       bf16x8 kf[KS], vf[KS];
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
@@ -349,62 +301,6 @@ __global__ __launch_bounds__(256, QCfg<D>::MINB) void attn_bwd_q_kernel(const pi
       }
     }
   };
-#else
-  auto tile = [&](const char* kb, bool mask, int n0) __attribute__((always_inline)) {
-    const char* vb = kb + C::IMG;
-    bf16x8 kf[2][KS], vf[2][KS];
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        kf[kt][ks] = lds_read_b128(kb, ro[ks] + kt * 32 * RB);
-        vf[kt][ks] = lds_read_b128(vb, ro[ks] + kt * 32 * RB);
-      }
-    // lane = query my_q; register i of half kt = key n0 + 32 kt + acc_row(i, h). The mask enters as the C
-    // operand of each S chain's first MFMA (as in attn_bwd_kv_kernel), keeping the tile one basic block.
-    f32x16 s[2], dp[2];
-    if (mask) {  // wave-uniform: diagonal / partial tiles only
-      const int rel = lim_lane - n0 - 4 * h;  // key allowed iff (32 kt + (i&3) + 8 (i>>2)) <= rel
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt) {
-        f32x16 m;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) m[i] = (32 * kt + (i & 3) + 8 * (i >> 2)) <= rel ? 0.f : -INFINITY;
-        s[kt] = mfma32(kf[kt][0], qf[0], m);
-      }
-    } else {
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt) s[kt] = mfma32(kf[kt][0], qf[0], (f32x16)0.f);
-    }
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
-#pragma unroll
-      for (int ks = 1; ks < KS; ++ks) s[kt] = mfma32(kf[kt][ks], qf[ks], s[kt]);
-      dp[kt] = mfma32(vf[kt][0], df[0], ndelta);
-#pragma unroll
-      for (int ks = 1; ks < KS; ++ks) dp[kt] = mfma32(vf[kt][ks], df[ks], dp[kt]);
-    }
-    bf16x8 dsf[2][2];
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
-      float ds[16];
-#pragma unroll
-      for (int i = 0; i < 16; ++i) ds[i] = fast_exp2(__builtin_fmaf(s[kt][i], scale_log2, nl2)) * dp[kt][i];
-      dsf[kt][0] = pack_bf16x8(ds);
-      dsf[kt][1] = pack_bf16x8(ds + 8);
-    }
-    // dQ^T[d][q] += K^T[d][key] dS^T[key][q]: A = transposed reads of the K image
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-      for (int st = 0; st < 2; ++st) {
-        const char* rowb = kb + (32 * kt + 16 * st) * RB;
-#pragma unroll
-        for (int dt = 0; dt < DT; ++dt) dq[dt] = mfma32(tr_pair(rowb, tro[dt][0], tro[dt][1]), dsf[kt][st], dq[dt]);
-      }
-  };
-
-#endif
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // prologue tiles and loads landed
 #if PICO_BWDQ_WGSTAMP
   wgs[1] = __builtin_amdgcn_s_memrealtime();
@@ -489,7 +385,7 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kv_kernel(const pico_
                                                               const float* __restrict__ lse2_g,
                                                               const float* __restrict__ delta_g, int sq_pad,
                                                               int hsplit, float* __restrict__ dkv_part,
-                                                              unsigned long long* __restrict__ stamp_out, int nfront) {
+                                                              unsigned long long* __restrict__ stamp_out) {
   using C = KVCfg<D>;
   constexpr int KS = C::KS, DT = C::DT, CPR = C::CPR, RB = C::RB;
   __shared__ __attribute__((aligned(16))) char smem[C::NBUF * C::SLOT];
@@ -505,13 +401,11 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kv_kernel(const pico_
   wgs[0] = __builtin_amdgcn_s_memrealtime();
 #endif
 
-  // heaviest key blocks first (causal: block 0 sees every query); small grids split a key block's
-  // (query head, query tile) list over `hsplit` workgroups with fp32 partials (attn_bwd_dkv_kernel sums)
+  // heaviest key blocks first (causal: block 0 sees every query; lightest-first fronts as in the dQ kernel
+  // measured neutral here); small grids split a key block's (query head, query tile) list over `hsplit`
+  // workgroups with fp32 partials (attn_bwd_dkv_kernel sums)
   const int nbh = (int)(a.batch * a.heads_kv) * hsplit;
-  // causal: the `nfront` lightest key blocks first, then heaviest-first (as attn_bwd_q_kernel's query blocks)
-  const int nkb = (Sk + KVB - 1) / KVB;
-  const int gi = blockIdx.x / nbh;
-  const int kb = (CAUSAL && gi < nfront) ? nkb - 1 - gi : gi - (CAUSAL ? nfront : 0);
+  const int kb = blockIdx.x / nbh;
   const int bhs = blockIdx.x % nbh;
   const int hs = bhs % hsplit;
   const int bh = bhs / hsplit;
@@ -661,17 +555,6 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kv_kernel(const pico_
   __builtin_amdgcn_s_waitcnt(0xC07F);
 #endif
 
-#if PICO_BWDKV_STAMP
-  __shared__ unsigned long long stamps[KNW * STAMP_T * STAMP_P];
-  auto stamp = [&](int t, int ph) __attribute__((always_inline)) {
-    __builtin_amdgcn_sched_barrier(0);
-    const unsigned long long v = __builtin_amdgcn_s_memtime();
-    if (lane == 0 && t < STAMP_T) stamps[(wave * STAMP_T + t) * STAMP_P + ph] = v;
-    __builtin_amdgcn_sched_barrier(0);
-  };
-#else
-  auto stamp = [](int, int) __attribute__((always_inline)) {};
-#endif
   // One 32-query tile = M1 (S = Q K^T and dP = dO V^T - delta: 8 MFMAs, mask and -delta in the C operand),
   // then V (P = exp2(S scale log2e - LSE log2e), dS = P dP: VALU) and M2 (dV^T += dO^T P, dK^T += Q^T dS:
   // 8 MFMAs with the packed accumulators as B operands). A tile wholly above the wave's keys (causal) is
@@ -684,7 +567,6 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kv_kernel(const pico_
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       qa[ks] = lds_read_b128(qs, qo[ks]);
-      if (!PICO_KV_SEQM1) da[ks] = lds_read_b128(dos, qo[ks]);
     }
     f32x16 nd;  // rows of this lane's accumulator registers: q = q0 + 8 g + 4 h + (0..3)
 #pragma unroll
@@ -710,8 +592,8 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kv_kernel(const pico_
 #pragma unroll
       for (int kt = 0; kt < KH; ++kt) s[kt] = mfma32(qa[0], kf[kt][0], (f32x16)0.f);
     }
-#if PICO_KV_SEQM1
-    // the dO fragments are read once the S chain has consumed Q's (16 fewer live VGPRs: room for MINB 3)
+    // the dO fragments are read once the S chain has consumed Q's (16 fewer live VGPRs: room for a third
+    // workgroup per CU; C2 58.5 -> 56.1 us at two)
 #pragma unroll
     for (int kt = 0; kt < KH; ++kt)
 #pragma unroll
@@ -725,17 +607,8 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kv_kernel(const pico_
 #pragma unroll
       for (int ks = 1; ks < KS; ++ks) dp[kt] = mfma32(da[ks], vf[kt][ks], dp[kt]);
     }
-#else
-#pragma unroll
-    for (int kt = 0; kt < KH; ++kt) {
-#pragma unroll
-      for (int ks = 1; ks < KS; ++ks) s[kt] = mfma32(qa[ks], kf[kt][ks], s[kt]);
-      dp[kt] = mfma32(da[0], vf[kt][0], nd);
-#pragma unroll
-      for (int ks = 1; ks < KS; ++ks) dp[kt] = mfma32(da[ks], vf[kt][ks], dp[kt]);
-    }
-#endif
   };
+  // V: P = exp2  };
   // V: P = exp2(S scale log2e - LSE log2e), dS = P dP, packed to bf16 (the B operands of M2)
   auto vsm = [&](int si, const f32x16 (&s)[KH], const f32x16 (&dp)[KH], bf16x8 (&pf)[KH][2], bf16x8 (&sf)[KH][2])
       __attribute__((always_inline)) {
@@ -775,162 +648,37 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kv_kernel(const pico_
       }
   };
 
-#if PICO_KV_PIPE
-  // Software pipeline across tiles inside each wave: the interval of tile t (between two barriers) holds
-  // M1 of tile t + 1 and V + M2 of tile t, independent work in one basic block; sched_group_barrier
-  // spreads the softmax VALU of tile t between the S / dP MFMAs of tile t + 1. S / dP of the next tile
-  // are carried across the barrier in two alternating register sets (4-slot ring, unrolled by 4).
-  int q0cur = q00;
-  auto step = [&](auto uc, int t0, f32x16 (&sc)[KH], f32x16 (&dpc)[KH], f32x16 (&sn)[KH], f32x16 (&dpn)[KH])
-      __attribute__((always_inline)) -> bool {
-    constexpr int u = decltype(uc)::value;
-    const int t = t0 + u;
-    if (t >= ntiles) return false;
-    const int q0n = q0cur + QT >= qend ? qstart : q0cur + QT;
-    if (t + 1 < ntiles) {
-      // this wave's pieces of tile t + 1 landed (tile t + 2's may stay in flight)
-      if (t + 2 < ntiles) {
-        if (wave < C::NP % KNW) wait_vmcnt(C::NP / KNW + 1);
-        else wait_vmcnt(C::NP / KNW);
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      lds_barrier();  // everyone's pieces of tile t + 1 visible; slot (t + 3) % NBUF (tile t - 1) unread
-    }
-    if (t + PD < ntiles) issue((u + PD) % C::NBUF, nxt);
-    advance(nxt);
-    // S / dP of tile t + 1 (after the last tile: of a stale slot, discarded — keeps the body branch-free)
-    // interleaved by hand with V of tile t: fenced slices of {one M1 MFMA, two softmax elements}
-    static_assert(KH == 1, "the hand-interleaved body is written for 32 keys per wave");
-    constexpr int sn_slot = (u + 1) % C::NBUF;
-    const char* qs = smem + sn_slot * C::SLOT;
-    const char* cs = smem + u * C::SLOT;  // tile t
-    const float* lsd_c = (const float*)(cs + 2 * C::QIMG);
-    const float* lsd_n = (const float*)(qs + 2 * C::QIMG);
-    f32x4 l2[4];
-#pragma unroll
-    for (int g = 0; g < 4; ++g) l2[g] = *reinterpret_cast<const f32x4*>(lsd_c + 8 * g + 4 * h);
-    bf16x8 qa[KS], da[KS];
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      qa[ks] = lds_read_b128(qs, qo[ks]);
-      da[ks] = lds_read_b128(qs + C::QIMG, qo[ks]);
-    }
-    f32x16 nd;
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const f32x4 v = *reinterpret_cast<const f32x4*>(lsd_n + 32 + 8 * g + 4 * h);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) nd[4 * g + j] = v[j];
-    }
-    if ((CAUSAL && kw + KPW - 1 > q0n) || kpad) {
-      const int key = kw + r;
-      const int rel = key >= Sk ? 64 : (CAUSAL ? key - q0n - 4 * h : -1);
-      f32x16 m;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) m[i] = ((i & 3) + 8 * (i >> 2) < rel) ? -INFINITY : 0.f;
-      sn[0] = mfma32(qa[0], kf[0][0], m);
-    } else {
-      sn[0] = mfma32(qa[0], kf[0][0], (f32x16)0.f);
-    }
-    float pv[16], sv[16];
-    bf16x8 pf[2], sf[2];
-    auto velem = [&](int i) __attribute__((always_inline)) {
-      pv[i] = fast_exp2(__builtin_fmaf(sc[0][i], scale_log2, -l2[i >> 2][i & 3]));
-      sv[i] = pv[i] * dpc[0][i];
-    };
-    bf16x8 dot[2][DT], qt[2][DT];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      __builtin_amdgcn_sched_barrier(0);
-      // M1 MFMAs 2..8 in slices 0..6: S ks = 1..KS-1, then the dP chain ks = 0..KS-1 (slice 7: none)
-      if (i < KS - 1) sn[0] = mfma32(qa[i + 1], kf[0][i + 1], sn[0]);
-      else if (i == KS - 1) dpn[0] = mfma32(da[0], vf[0][0], nd);
-      else if (i < 2 * KS - 1) dpn[0] = mfma32(da[i - KS + 1], vf[0][i - KS + 1], dpn[0]);
-      velem(2 * i);
-      velem(2 * i + 1);
-      if (i == 3) {
-        pf[0] = pack_bf16x8(pv);
-        sf[0] = pack_bf16x8(sv);
-      }
-      if (i >= 4) {  // M2's transposed operands, one (st, dt) pair per slice
-        const int st = (i - 4) >> 1, dt = (i - 4) & 1;
-        dot[st][dt] = tr_pair(cs + C::QIMG + 16 * st * RB, tro[dt][0], tro[dt][1]);
-        qt[st][dt] = tr_pair(cs + 16 * st * RB, tro[dt][0], tro[dt][1]);
-      }
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    pf[1] = pack_bf16x8(pv + 8);
-    sf[1] = pack_bf16x8(sv + 8);
-#pragma unroll
-    for (int st = 0; st < 2; ++st)
-#pragma unroll
-      for (int dt = 0; dt < DT; ++dt) {
-        dv[dt][0] = mfma32(dot[st][dt], pf[st], dv[dt][0]);
-        dk[dt][0] = mfma32(qt[st][dt], sf[st], dk[dt][0]);
-      }
-    q0cur = q0n;
-    return true;
-  };
-  f32x16 sA[KH], dA[KH], sB[KH], dB[KH];  // S / dP register sets: even tiles in A, odd tiles in B
-  if (ntiles > 0) m1(0, q00, sA, dA);
-  for (int t0 = 0; t0 < ntiles; t0 += C::NBUF) {
-    static_assert(C::NBUF == 4, "the unrolled body below assumes a 4-slot ring");
-    if (!step(std::integral_constant<int, 0>{}, t0, sA, dA, sB, dB)) break;
-    if (!step(std::integral_constant<int, 1>{}, t0, sB, dB, sA, dA)) break;
-    if (!step(std::integral_constant<int, 2>{}, t0, sA, dA, sB, dB)) break;
-    if (!step(std::integral_constant<int, 3>{}, t0, sB, dB, sA, dA)) break;
-  }
-#else
   // Unrolled by the ring depth: the slot of every LDS read is a compile-time constant (immediate offsets).
-  // R tiles per barrier interval: one counted wait, one barrier and one DMA issue round serve R tiles.
   // (Measured and dropped, C2 causal: a stagger of the two waves of each SIMD by one phase — +2 %; carrying
   // S / dP of tile t + 1 across the barrier so M1(t + 1) overlaps V(t) inside the wave — +6 %.)
-  constexpr int R = C::R;
   constexpr int NPMY_LO = C::NP / KNW;  // this wave's pieces per tile: NPMY_LO or NPMY_LO + 1
   int q0cur = q00;
   for (int t0 = 0; t0 < ntiles; t0 += C::NBUF) {
 #pragma unroll
-    for (int u = 0; u < C::NBUF; u += R) {
+    for (int u = 0; u < C::NBUF; ++u) {
       const int t = t0 + u;
       if (t >= ntiles) break;
-      stamp(t, 0);
       if (t > 0) {
-        // this wave's pieces of tiles t .. t + R - 1 landed; the next interval's R tiles may stay in flight
-        if (t + 2 * R <= ntiles) {
-          if (wave < C::NP % KNW) wait_vmcnt(R * (NPMY_LO + 1));
-          else wait_vmcnt(R * NPMY_LO);
+        // this wave's pieces of tile t landed; the next tile's may stay in flight
+        if (t + 2 <= ntiles) {
+          if (wave < C::NP % KNW) wait_vmcnt(NPMY_LO + 1);
+          else wait_vmcnt(NPMY_LO);
         } else {
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
-        lds_barrier();  // everyone's pieces visible; slots of tiles t - R .. t - 1 no longer read
+        lds_barrier();  // everyone's pieces visible; the slot of tile t - 1 is no longer read
       }
-      stamp(t, 1);
-#pragma unroll
-      for (int i = 0; i < R; ++i) {
-        if (t + PD + i < ntiles) issue((u + PD + i) % C::NBUF, nxt);
-        advance(nxt);
-      }
-      stamp(t, 2);
-#pragma unroll
-      for (int i = 0; i < R; ++i) {
-        if (i > 0 && t + i >= ntiles) break;
-        f32x16 s[KH], dp[KH];
-        bf16x8 pf[KH][2], sf[KH][2];
-        m1(u + i, q0cur, s, dp);
-        vsm(u + i, s, dp, pf, sf);
-        m2(u + i, pf, sf);
-        q0cur = q0cur + QT >= qend ? qstart : q0cur + QT;
-      }
-      stamp(t, 4);
+      if (t + PD < ntiles) issue((u + PD) % C::NBUF, nxt);
+      advance(nxt);
+      f32x16 s[KH], dp[KH];
+      bf16x8 pf[KH][2], sf[KH][2];
+      m1(u, q0cur, s, dp);
+      vsm(u, s, dp, pf, sf);
+      m2(u, pf, sf);
+      q0cur = q0cur + QT >= qend ? qstart : q0cur + QT;
     }
   }
 
-#endif
-#if PICO_BWDKV_STAMP
-  if (blockIdx.x == 0)
-    for (int i = lane; i < STAMP_T * STAMP_P; i += 64) stamp_out[wave * STAMP_T * STAMP_P + i] = stamps[wave * STAMP_T * STAMP_P + i];
-#endif
 #if PICO_BWDKV_WGSTAMP
   wgs[2] = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -1003,11 +751,13 @@ int64_t split_lsd_floats(const pico_attn_args* a) {
   return ((n + 63) / 64) * 64;
 }
 
-// dK/dV workgroups per CU (see PICO_KV_MINB): 3 for causal grids, 2 for non-causal ones (whose mask-free
-// body does not fit 168 VGPRs without spills either)
+// dK/dV workgroups per CU the register budget is sized for: 3 (168 VGPRs) for causal grids, whose LPT-ordered
+// uneven blocks fill any number of slots (C2 58.5 -> 52.6 us, S 4096 153 -> 143); 2 (256 VGPRs) for non-causal
+// grids, whose equal blocks would leave a third round partly empty (C2 full: 1024 blocks = 2 rounds of 512 slots
+// vs 1.33 rounds of 768) and whose mask-free body spills at 168 VGPRs (83 vs 123 us); 1 at D = 128 (≈ 340
+// registers: its own translation unit, AGPRs allowed).
 int kv_minb(const pico_attn_args* a) {
-  if (a->head_dim == 128) return 1;  // ≈ 340 registers (its own translation unit, AGPRs allowed)
-  if (PICO_KV_MINB) return PICO_KV_MINB;
+  if (a->head_dim == 128) return 1;
   return a->causal ? 3 : 2;
 }
 
@@ -1027,51 +777,13 @@ int kv_hsplit(const pico_attn_args* a) {
 int64_t pico_attn_bwd_split_workspace(const pico_attn_args* a);
 namespace {
 
-// dQ kernel: query blocks dispatched lightest-first (see attn_bwd_q_kernel); PICO_BWDQ_FRONT < 0: automatic
-#ifndef PICO_BWDQ_FRONT
-#define PICO_BWDQ_FRONT -1
-#endif
+// dQ kernel: query blocks dispatched lightest-first (see attn_bwd_q_kernel)
 int q_front(const pico_attn_args* a) {
   if (!a->causal) return 0;
   const int nmb = (int)((a->seqlen_q + QB - 1) / QB);
-  if (PICO_BWDQ_FRONT >= 0) return PICO_BWDQ_FRONT < nmb ? PICO_BWDQ_FRONT : nmb;
   const int64_t nbh = a->batch * a->heads_q;
   const int64_t first = (int64_t)pico_num_cus() * (a->head_dim == 64 ? QCfg<64>::MINB : QCfg<128>::MINB) /
                         (nbh > 0 ? nbh : 1);  // groups resident at once
-  return first < nmb ? (int)(nmb - first) : 0;
-}
-
-// PICO_KV_FRONT: the dQ kernel's lightest-first front groups for the dK/dV kernel (-1 automatic, as q_front).
-// Measured neutral (C2 55.8 -> 54.5 us, GQA-4 equal, S 4096 145.5 -> 147.5; 4 rounds): off.
-#ifndef PICO_KV_FRONT
-#define PICO_KV_FRONT 0
-#endif
-int kv_front(const pico_attn_args* a, int hsplit) {
-  if (!a->causal) return 0;
-  const int nkb = (int)((a->seqlen_k + KVB - 1) / KVB);
-  if (PICO_KV_FRONT >= 0) return PICO_KV_FRONT < nkb ? PICO_KV_FRONT : nkb;
-  const int64_t nbh = a->batch * a->heads_kv * hsplit;
-  const int64_t first = (int64_t)pico_num_cus() * kv_minb(a) / (nbh > 0 ? nbh : 1);
-  return first < nkb ? (int)(nkb - first) : 0;
-}
-
-}  // namespace
-bool pico_attn_bwd_q64_ok(const pico_attn_args* a);  // attn_bwd_q64.hip
-int pico_attn_bwd_q64(const pico_attn_args* a, hipStream_t s, float* lse2, float* delta, int sq_pad, int nfront);
-namespace {
-// D = 64 dQ: the tile-pipelined kernel (attn_bwd_q64.hip) when PICO_ATTN_BWDQ64=1 (A/B against attn_bwd_q_kernel)
-bool use_bwdq64() {
-  static const int on = [] {
-    const char* e = getenv("PICO_ATTN_BWDQ64");
-    return e && e[0] == '1' ? 1 : 0;
-  }();
-  return on != 0;
-}
-int q_front_minb(const pico_attn_args* a, int minb) {
-  if (!a->causal) return 0;
-  const int nmb = (int)((a->seqlen_q + QB - 1) / QB);
-  const int64_t nbh = a->batch * a->heads_q;
-  const int64_t first = (int64_t)pico_num_cus() * minb / (nbh > 0 ? nbh : 1);
   return first < nmb ? (int)(nmb - first) : 0;
 }
 
@@ -1085,26 +797,24 @@ int launch_split(const pico_attn_args* a, hipStream_t s) {
   const int nmb = (int)((a->seqlen_q + QB - 1) / QB);
   const int64_t gq = (int64_t)nmb * a->batch * a->heads_q;
   PICO_REQUIRE(gq < (1ll << 31), "pico_attn_bwd: grid too large");
-  if (D == 64 && use_bwdq64() && pico_attn_bwd_q64_ok(a)) {
-    PICO_TRY(pico_attn_bwd_q64(a, s, lse2, delta, sq_pad, q_front_minb(a, 2)));
-  } else {
-    PICO_TRY(pico_launch(PICO_K_ATTN_BWD_Q, "attn_bwd_q", attn_bwd_q_kernel<D, CAUSAL>, dim3((int)gq), dim3(256), 0, s, *a, a->softmax_scale, sl2, lse2, delta, sq_pad,
-                    (unsigned long long*)((char*)a->workspace + pico_attn_bwd_split_workspace(a) - STAMP_BYTES),
-                    q_front(a)));
-  }
+  PICO_TRY(pico_launch(PICO_K_ATTN_BWD_Q, "attn_bwd_q", attn_bwd_q_kernel<D, CAUSAL>, dim3((int)gq), dim3(256), 0, s,
+                       *a, a->softmax_scale, sl2, lse2, delta, sq_pad,
+                       (unsigned long long*)((char*)a->workspace + pico_attn_bwd_split_workspace(a) - STAMP_BYTES),
+                       q_front(a)));
   const int nkb = (int)((a->seqlen_k + KVB - 1) / KVB);
   const int hsplit = kv_hsplit(a);
   const int64_t nblk = (int64_t)nkb * a->batch * a->heads_kv * hsplit;
   if (nblk == 0) return 0;
   unsigned long long* stamps = (unsigned long long*)((char*)a->workspace + pico_attn_bwd_split_workspace(a) - STAMP_BYTES);
   if constexpr (D == 128) {
-    PICO_TRY(pico_launch(PICO_K_ATTN_BWD_KV, "attn_bwd_kv", attn_bwd_kv_kernel<D, CAUSAL, 1>, dim3((int)nblk), dim3(KNW * 64), 0, s, *a, a->softmax_scale, sl2, lse2, delta, sq_pad, hsplit, dkv_part, stamps, kv_front(a, hsplit)));
-  } else if (kv_minb(a) == 1) {  // PICO_KV_MINB=1 (A/B): one workgroup per CU, the whole register file
-    PICO_TRY(pico_launch(PICO_K_ATTN_BWD_KV, "attn_bwd_kv", attn_bwd_kv_kernel<D, CAUSAL, 1>, dim3((int)nblk), dim3(KNW * 64), 0, s, *a, a->softmax_scale, sl2, lse2, delta, sq_pad, hsplit, dkv_part, stamps, kv_front(a, hsplit)));
-  } else if (CAUSAL && kv_minb(a) == 3) {
-    PICO_TRY(pico_launch(PICO_K_ATTN_BWD_KV, "attn_bwd_kv", attn_bwd_kv_kernel<D, CAUSAL, 3>, dim3((int)nblk), dim3(KNW * 64), 0, s, *a, a->softmax_scale, sl2, lse2, delta, sq_pad, hsplit, dkv_part, stamps, kv_front(a, hsplit)));
+    PICO_TRY(pico_launch(PICO_K_ATTN_BWD_KV, "attn_bwd_kv", attn_bwd_kv_kernel<D, CAUSAL, 1>, dim3((int)nblk),
+                         dim3(KNW * 64), 0, s, *a, a->softmax_scale, sl2, lse2, delta, sq_pad, hsplit, dkv_part, stamps));
+  } else if (CAUSAL) {
+    PICO_TRY(pico_launch(PICO_K_ATTN_BWD_KV, "attn_bwd_kv", attn_bwd_kv_kernel<D, CAUSAL, 3>, dim3((int)nblk),
+                         dim3(KNW * 64), 0, s, *a, a->softmax_scale, sl2, lse2, delta, sq_pad, hsplit, dkv_part, stamps));
   } else {
-    PICO_TRY(pico_launch(PICO_K_ATTN_BWD_KV, "attn_bwd_kv", attn_bwd_kv_kernel<D, CAUSAL, 2>, dim3((int)nblk), dim3(KNW * 64), 0, s, *a, a->softmax_scale, sl2, lse2, delta, sq_pad, hsplit, dkv_part, stamps, kv_front(a, hsplit)));
+    PICO_TRY(pico_launch(PICO_K_ATTN_BWD_KV, "attn_bwd_kv", attn_bwd_kv_kernel<D, CAUSAL, 2>, dim3((int)nblk),
+                         dim3(KNW * 64), 0, s, *a, a->softmax_scale, sl2, lse2, delta, sq_pad, hsplit, dkv_part, stamps));
   }
   if (hsplit > 1) {
     const int kv_blocks = pico_cdiv(a->batch * a->seqlen_k * a->heads_kv * (D / 16), 256);

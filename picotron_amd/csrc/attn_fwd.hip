@@ -54,20 +54,10 @@
 #ifndef PICO_FWD_WGSTAMP
 #define PICO_FWD_WGSTAMP 0
 #endif
-// PICO_FWD_NOWAIT: ablation build (results wrong, timing only) -- the loop never waits for its K/V DMA: the
-// time the per-tile vmcnt waits cost
-#ifndef PICO_FWD_NOWAIT
-#define PICO_FWD_NOWAIT 0
-#endif
-
 // PICO_FWD_SNAKE: causal block order. The grid is dispatched in rounds of one workgroup per CU; when every
 // workgroup is resident at once (C2: 1024 = 4 per CU) each CU keeps the blocks one round hands it, so a
 // plain heaviest-first order gives the CUs that take the heaviest block of every round 40 tiles and the
 // others 32. Odd rounds run lightest-first instead (a snake over the sorted list): 36 tiles on every CU.
-// PICO_FWD_PRIO: s_setprio level around each MFMA burst (0 = off). Measured C2 32.4 -> 32.7 us at 1 or 3.
-#ifndef PICO_FWD_PRIO
-#define PICO_FWD_PRIO 0
-#endif
 #ifndef PICO_FWD_SNAKE
 #define PICO_FWD_SNAKE 1
 #endif
@@ -269,22 +259,6 @@ __attribute__((amdgpu_waves_per_eu(FwdCfg<D>::WAVES_PER_EU, FwdCfg<D>::WAVES_PER
       });
     });
   };
-  // PICO_FWD_PRIO: raise the wave's issue priority around its MFMA bursts (the matrix pipe is fed first,
-  // the co-resident waves' softmax VALU fills the gaps)
-  auto prio_up = [&]() __attribute__((always_inline)) {
-    if (PICO_FWD_PRIO) {
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_setprio(PICO_FWD_PRIO);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  };
-  auto prio_down = [&]() __attribute__((always_inline)) {
-    if (PICO_FWD_PRIO) {
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_setprio(0);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  };
   // P^T (keys 32 kt .. 32 kt + 31 of the tile) times V: 2 * DT MFMAs.
   auto pv_mfma = [&](const f32x16& p, const bf16x8 (&vf)[2][DT]) __attribute__((always_inline)) {
     float pv[16];
@@ -292,12 +266,10 @@ __attribute__((amdgpu_waves_per_eu(FwdCfg<D>::WAVES_PER_EU, FwdCfg<D>::WAVES_PER
     for (int j = 0; j < 16; ++j) pv[j] = p[j];
     const bf16x8 pf0 = pack_bf16x8(pv), pf1 = pack_bf16x8(pv + 8);  // one v_cvt_pk_bf16_f32 per pair
     lds_wait_all();
-    prio_up();
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) o[dt] = mfma32(vf[0][dt], pf0, o[dt]);
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) o[dt] = mfma32(vf[1][dt], pf1, o[dt]);
-    prio_down();
   };
 
   // S^T of one 64-key tile (2 x 16 accumulators), masked when MASK
@@ -308,7 +280,6 @@ __attribute__((amdgpu_waves_per_eu(FwdCfg<D>::WAVES_PER_EU, FwdCfg<D>::WAVES_PER
     for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) kf[kt][ks] = lds_read_b128(kb, ks * C::KIMG + kt * 32 * 32);
-    prio_up();
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
       s[kt] = (f32x16)0.f;
@@ -317,7 +288,6 @@ __attribute__((amdgpu_waves_per_eu(FwdCfg<D>::WAVES_PER_EU, FwdCfg<D>::WAVES_PER
     }
     __builtin_amdgcn_sched_group_barrier(0x100, 2 * KS, 0);  // the K reads first,
     __builtin_amdgcn_sched_group_barrier(0x008, 2 * KS, 0);  // then the S MFMAs
-    prio_down();
     // lane holds row my_q, keys n0 + 32 kt + acc_row(i, h) = n0 + 4h + c(kt, i)
     if (mask) {  // wave-uniform
       const int rel = lim_lane - n0 - 4 * h;  // key allowed iff c <= rel
@@ -411,8 +381,7 @@ __attribute__((amdgpu_waves_per_eu(FwdCfg<D>::WAVES_PER_EU, FwdCfg<D>::WAVES_PER
 #endif
   for (int t = 0; t < ntiles; ++t) {
     // tile t's pieces landed (this wave's), then every wave's (barrier); later tiles stay in flight
-    if (PICO_FWD_NOWAIT) {  // ablation (results wrong, timing only): no wait for the tile's DMA
-    } else if (P == 2 && t + 1 < ntiles) {
+    if (P == 2 && t + 1 < ntiles) {
       if constexpr (C::NIW == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     } else {
@@ -509,19 +478,6 @@ int launch_fwd(const pico_attn_args* a, hipStream_t s) {
 }  // namespace
 
 int pico_attn_check_common(const pico_attn_args* a, const char* op);
-bool pico_attn_fwd64_pp_ok(const pico_attn_args* a);         // attn_fwd64.hip
-int pico_attn_fwd64_pp(const pico_attn_args* a, hipStream_t s);
-
-// D = 64: the ping-pong kernel (attn_fwd64.hip) when PICO_ATTN_FWD64=1 (A/B against this file's 128-row
-// kernel; not the default until it is faster in the training step)
-static bool use_fwd64() {
-  static const int on = [] {
-    const char* e = getenv("PICO_ATTN_FWD64");
-    return e && e[0] == '1' ? 1 : 0;
-  }();
-  return on != 0;
-}
-
 extern "C" int pico_attn_fwd(const pico_attn_args* a, void* stream) {
   int rc = pico_attn_check_common(a, "pico_attn_fwd");
   if (rc) return rc;
@@ -538,9 +494,6 @@ extern "C" int pico_attn_fwd(const pico_attn_args* a, void* stream) {
   }
   if (a->batch == 0 || a->seqlen_q == 0 || a->heads_q == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
-  if (a->head_dim == 64) {
-    if (use_fwd64() && pico_attn_fwd64_pp_ok(a)) return pico_attn_fwd64_pp(a, s);
-    return launch_fwd<64>(a, s);
-  }
+  if (a->head_dim == 64) return launch_fwd<64>(a, s);
   return launch_fwd<128>(a, s);
 }

@@ -29,10 +29,12 @@ def synth_tokens(n_rows, seq_plus_one, vocab, generator, kind="uniform"):
 
 class SyntheticDataLoader:
     def __init__(self, micro_batch_size, seq_length, grad_acc_steps, vocab_size, seed=1234, kind="uniform",
-                 num_batches=None, device="cpu"):
+                 num_batches=None, device="cpu", dp_rank=None):
+        """dp_rank: the data-parallel rank whose stream to produce (default: this process's, from the process
+        group manager) — a one-process check can replay every rank's micro-batches."""
         m = pgm.process_group_manager
         self.dp_world_size = m.dp_world_size if m is not None else 1
-        self.dp_rank = m.dp_rank if m is not None else 0
+        self.dp_rank = dp_rank if dp_rank is not None else (m.dp_rank if m is not None else 0)
         self.cp_world_size = m.cp_world_size if m is not None else 1
         self.cp_rank = m.cp_rank if m is not None else 0
         self.micro_batch_size = micro_batch_size

@@ -14,6 +14,7 @@ register_post_accumulate_grad_hook is the same event) run on the autograd device
     `.grad` views.
 """
 import contextlib
+import weakref
 
 import torch
 import torch.distributed as dist
@@ -54,18 +55,38 @@ class DataParallelNaive(nn.Module):
         self.require_backward_grad_sync = True
 
 
+# DataParallelBucket wrappers with defer_grad_cast=True. A global optimizer step pre-hook runs their deferred
+# fp32 -> bf16 .grad cast before any optimizer that does not read the fp32 main_grad itself (everything but
+# picotron_amd.optim.AdamW) steps, so torch.optim optimizers see the same .grad as with the eager cast.
+_DEFERRING = weakref.WeakSet()
+_DEFER_HOOK = []
+
+
+def _materialize_before_foreign_step(optimizer, args, kwargs):
+    if getattr(optimizer, "reads_deferred_grads", False):
+        return
+    for dp in list(_DEFERRING):
+        dp.materialize_grads()
+
+
 class DataParallelBucket(nn.Module):
 
     def __init__(self, module, bucket_cap_mb=25, grad_type=torch.float32, defer_grad_cast=False):
         """ref :62-85. defer_grad_cast (an extension, off by default): after a syncing backward `.grad` is the
         bucket's bf16 view WITHOUT the fp32 -> bf16 cast of ref :165 having run; picotron_amd.optim.AdamW reads
         the averaged fp32 main_grad instead and rounds it to bf16 in register exactly as the cast would
-        (bit-identical step, no bf16 .grad write + re-read: 4 B per parameter per step). Anything else that
-        reads `.grad` must call materialize_grads() first."""
+        (bit-identical step, no bf16 .grad write + re-read: 4 B per parameter per step). Any other optimizer gets
+        the cast run for it by a step pre-hook before it steps; code that reads `.grad` outside an optimizer step
+        (clip_grad_norm_, grad-norm logging, checkpointing grads) must call materialize_grads() first."""
         super().__init__()
         self.module = module
         self.require_backward_grad_sync = True
         self.defer_grad_cast = bool(defer_grad_cast)
+        if self.defer_grad_cast:
+            _DEFERRING.add(self)
+            if not _DEFER_HOOK:
+                from torch.optim.optimizer import register_optimizer_step_pre_hook
+                _DEFER_HOOK.append(register_optimizer_step_pre_hook(_materialize_before_foreign_step))
         grad_size = 2 if grad_type == torch.bfloat16 else 4
         bucket_size = bucket_cap_mb * 1024 * 1024 // grad_size
         self.bucket_manager = BucketManager(module.parameters(), pgm.process_group_manager.cp_dp_group, bucket_size,
@@ -76,10 +97,12 @@ class DataParallelBucket(nn.Module):
         self._post_backward_callback_set = False
 
     def forward(self, *inputs, **kwargs):
-        # no backward pass is in flight while the host runs a forward: per-pass state left by a backward that
-        # raised midway (its end-of-pass callbacks never ran) is dropped here
-        self._end_pass()
-        self._post_backward_callback_set = False
+        # per-pass state left by a backward that raised midway (its end-of-pass callbacks never ran) is dropped
+        # here — unless this forward itself runs inside a backward pass (activation recompute, a
+        # forward from a hook), whose state is live
+        if torch._C._current_graph_task_id() == -1:
+            self._end_pass()
+            self._post_backward_callback_set = False
         return self.module(*inputs, **kwargs)
 
     def backward(self, input_tensor, output_tensor, output_tensor_grad):

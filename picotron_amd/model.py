@@ -54,6 +54,19 @@ def llama2_7b(num_hidden_layers=32, seq_length=4096):
                        rms_norm_eps=1e-5, rope_theta=10000.0)
 
 
+def require_kernel_path():
+    """The reference's FLASH_ATTEN switch (ref picotron/model.py:126,151,191,247; set from the config's
+    environment block, ref train.py:67): "1" (its default) runs the fused kernels, anything else the eager
+    LlamaRMSNorm / apply_rotary_pos_emb / SDPA path. This package is the kernel path only — there is no eager
+    path by design (north_star: no dual dispatch) — so FLASH_ATTEN != "1" is refused here instead of silently
+    running the gfx950 kernels. Checked where the reference reads it: at module construction (:191, :247) and
+    in Attention.forward (:126, :151)."""
+    v = os.getenv("FLASH_ATTEN", "1")
+    if v != "1":
+        raise RuntimeError(f"FLASH_ATTEN={v!r}: picotron_amd runs the gfx950 kernel path only (the reference's eager "
+                           "FLASH_ATTEN=0 path is not provided); unset FLASH_ATTEN or set it to 1")
+
+
 def _table_device():
     if os.getenv("DEVICE", "cuda") == "cuda" and torch.cuda.is_available():
         return torch.device("cuda", torch.cuda.current_device())
@@ -173,6 +186,7 @@ class Attention(nn.Module):
         return _col_parallel((self.q_proj, self.k_proj, self.v_proj))
 
     def forward(self, x, cos, sin, attention_mask=None, position_ids=None):
+        require_kernel_path()
         B, S, _ = x.size()
         D = self.head_dim
         kind = self._fusable()
@@ -229,6 +243,7 @@ class DecoderLayer(nn.Module):
 
     def __init__(self, config, layer_idx):
         super().__init__()
+        require_kernel_path()  # ref :191 picks the RMSNorm class from FLASH_ATTEN here
         self.input_layernorm = RMSNorm(config.hidden_size, eps=config.rms_norm_eps)
         self.post_attention_layernorm = RMSNorm(config.hidden_size, eps=config.rms_norm_eps)
         self.attention = Attention(config, layer_idx=layer_idx)
@@ -295,6 +310,7 @@ class Llama(nn.Module):
 
     def __init__(self, config) -> None:
         super().__init__()
+        require_kernel_path()  # ref :247
         assert config.hidden_size % config.num_attention_heads == 0
         assert config.num_attention_heads % config.num_key_value_heads == 0
         self.vocab_size = config.vocab_size

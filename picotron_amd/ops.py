@@ -45,9 +45,10 @@ class _RMSNormFn(torch.autograd.Function):
     def forward(ctx, x, residual, weight, eps, prenorm, want_t=False):
         _need(x, "x")
         _need(weight, "weight")
-        # a chained dw left pending means the backward pass that created it raised before its end-of-pass
-        # flush ran (no backward pass is in flight during a forward): drop it
-        if _NORM_PENDING:
+        # a chained dw left pending while no backward pass runs means the pass that created it raised before its
+        # end-of-pass flush ran: drop it. A forward inside a running backward (activation recompute,
+        # a forward from a hook) leaves it alone: that pass's next norm backward or its flush reduces it.
+        if _NORM_PENDING and not _backward_running():
             _NORM_PENDING.pop(x.device, None)
         shape = x.shape
         cols = shape[-1]
@@ -130,6 +131,11 @@ class _RMSNormFn(torch.autograd.Function):
 # (workspace, partial rows, cols, target, mode, scale, ready callback); _flush_norm_dw reduces what is left
 # when the backward pass ends
 _NORM_PENDING = {}
+
+
+def _backward_running():
+    """True on a thread that is executing an autograd backward pass (its graph task)."""
+    return torch._C._current_graph_task_id() != -1
 
 
 def _norm_chain_enabled():
@@ -377,48 +383,31 @@ def wgrad_accumulate(params, dy2, x2):
 # is seen:
 #   * an optimizer step (a global torch.optim step post-hook bumps a generation; the fused AdamW does not
 #     bump the parameters' version counters);
-#   * an in-place write through the parameter itself (`with no_grad(): p.copy_(x)`, load_state_dict): its
-#     version counter;
-#   * any access to a parameter's `.data` (p.data.copy_(x), p.data.mul_(2), p.data = t, module.to()): the
-#     `.data` property of torch.nn.Parameter is wrapped on first use of the cache to bump the generation
-#     (a write through `.data` bumps no version counter, and torch exposes no other hook for it). Every
-#     access counts as a possible write; the product path itself touches `.data` only at setup.
-#   * a parameter re-pointed at other storage: entries are keyed by the weight's storage and data pointer.
-# Not seen: a tensor obtained from `.data` earlier and written after the next use, and raw writes to
-# p.data_ptr() by foreign kernels; invalidate_weight_transposes() covers those. MicroBatchGraph calls
-# refresh_weight_transposes() before each replay (a replayed graph runs no host code). Entries hold their
-# parameters only through weak references: a rebuilt model does not keep the old one's weights alive.
+#   * an in-place write through the parameter itself (`with no_grad(): p.copy_(x)`, `load_state_dict`, which
+#     copies into the parameters): its version counter;
+#   * a parameter re-pointed at other storage (`p.data = t`, `module.to(other dtype / device)`): entries are
+#     keyed by the weight's storage and data pointer.
+# Not seen — and the one case that needs invalidate_weight_transposes(): an in-place write through a `.data`
+# alias (`p.data.copy_(x)`, `p.data.mul_(2)`; the alias has its own version counter) and raw writes to
+# p.data_ptr() by foreign kernels. Reading `.data` (logging, norms, EMA, deepcopy) costs nothing: no torch class
+# is patched. MicroBatchGraph calls refresh_weight_transposes() before each replay (a replayed graph runs no host
+# code). Entries hold their parameters only through weak references: a rebuilt model does not keep the old one's
+# weights alive.
 # --------------------------------------------------------------------------------------------
 _WT_GEN = [0]
 _WT_CACHE = {}  # (storage id, W.data_ptr(), shape) -> [wt, key, [weakref(p) for p in params]]
 _WT_HOOK = []
+_WT_STATS = {"transposes": 0}  # W^T (re)computations since import (tests: steady-state refresh count)
 
 
 def _bump_wt_gen(*_):
     _WT_GEN[0] += 1
 
 
-def _watch_parameter_data():
-    """Wrap torch.nn.Parameter.data (getter and setter) so that any `.data` access bumps the W^T generation."""
-    if getattr(torch.nn.Parameter, "_pico_data_watched", False):
-        return
-    desc = torch._C.TensorBase.__dict__["data"]
-
-    def _get(self):
-        _WT_GEN[0] += 1
-        return desc.__get__(self)
-
-    def _set(self, value):
-        _WT_GEN[0] += 1
-        desc.__set__(self, value)
-
-    torch.nn.Parameter.data = property(_get, _set, doc=desc.__doc__)
-    torch.nn.Parameter._pico_data_watched = True
-
-
 def invalidate_weight_transposes():
-    """Mark every cached W^T stale (re-transposed on next use). Not needed after optimizer steps, in-place
-    writes or `.data` writes (all detected); only after raw writes to a parameter's storage by foreign code."""
+    """Mark every cached W^T stale (re-transposed on next use). Optimizer steps, in-place writes through the
+    parameters and re-pointed parameters are detected; call this after writes through a `.data` alias
+    (`p.data.copy_(x)`) or raw writes to a parameter's storage by foreign code."""
     _bump_wt_gen()
 
 
@@ -440,7 +429,6 @@ def weight_t(W, params):
     """Contiguous W^T ([K, N] for W [N, K]), up to date with the parameters `params` W is made of."""
     if not _WT_HOOK:
         _WT_HOOK.append(_register_step_post_hook(_bump_wt_gen))
-        _watch_parameter_data()
     key = (_WT_GEN[0],) + tuple(p._version for p in params)
     ck = _wt_key(W)
     ent = _WT_CACHE.get(ck)
@@ -454,6 +442,7 @@ def weight_t(W, params):
         with torch.no_grad():
             transpose_2d(W, out=ent[0])
         ent[1] = key
+        _WT_STATS["transposes"] += 1
     return ent[0]
 
 

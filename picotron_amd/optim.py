@@ -25,6 +25,10 @@ def _deferred_grad(p):
 
 
 class AdamW(torch.optim.Optimizer):
+    # reads DataParallelBucket(defer_grad_cast=True)'s fp32 main_grad itself: the bucket's step pre-hook leaves
+    # the deferred cast to this optimizer (see data_parallel.py)
+    reads_deferred_grads = True
+
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, amsgrad=False, *,
                  maximize=False, foreach=None, capturable=False, differentiable=False, fused=None):
         if amsgrad or maximize or capturable or differentiable:

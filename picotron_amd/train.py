@@ -155,6 +155,50 @@ class MicroBatchGraph:
         return out
 
 
+class TrainingStep:
+    """One optimizer step of the reference loop (ref train.py:219-240) on this hot path, exactly as bench.py runs
+    it: optimizer.zero_grad(), train_step over grad_acc micro-batches (the non-syncing ones replayed from a HIP
+    graph when `graphs`; the syncing one eager, since its RCCL all-reduces launch from hooks), optimizer.step(),
+    model.reset(). The phases are exposed separately (zero / micro_batches / optimizer_step / reset) so tests can
+    inspect the gradients between them."""
+
+    def __init__(self, model, optimizer, loader, device, graphs=True):
+        self.model = model
+        self.optimizer = optimizer
+        self.loader = loader
+        self.device = device
+        self.graphs = MicroBatchGraph(model, loader.grad_acc_steps, self.zero_grads) if graphs else None
+
+    def zero_grads(self):
+        """Zero every gradient buffer in place (graph replays keep persistent buffers)."""
+        for p in self.model.parameters():
+            if p.grad is not None:
+                p.grad.zero_()
+        if hasattr(self.model, "bucket_manager"):
+            self.model.bucket_manager.reset()
+
+    def zero(self):
+        # graphs: gradient buffers must persist (zeroed in place); eager: the reference's set_to_none
+        self.optimizer.zero_grad(set_to_none=self.graphs is None)
+
+    def micro_batches(self, sync_loss=True):
+        return train_step(self.model, self.loader, self.device, graphs=self.graphs, sync_loss=sync_loss)
+
+    def optimizer_step(self):
+        self.optimizer.step()
+
+    def reset(self):
+        if hasattr(self.model, "reset"):
+            self.model.reset()
+
+    def __call__(self, sync_loss=True):
+        self.zero()
+        loss = self.micro_batches(sync_loss)
+        self.optimizer_step()
+        self.reset()
+        return loss
+
+
 def get_mfu(tokens_per_second_per_gpu, num_params, model_config, theoretical_flops=MI355X_BF16_PEAK):
     """ref picotron/utils.py:42-48 with the MI355X peak: 6N + 12*L*H*S FLOP per token."""
     flops_per_token = (6 * num_params + 12 * model_config.num_hidden_layers * model_config.hidden_size *

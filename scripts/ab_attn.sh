@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 for r in $(seq 1 ${ROUNDS:-3}); do
   for v in ${VARIANTS}; do
-    PICO_ATTN_FWD64=${PICO_ATTN_FWD64:-1} PICO_LIB_PATH=picotron_amd/lib/variants/$v.so timeout -k 10 120 python scripts/attn_bench.py --configs ${ATTN_CONFIGS:-c2} --iters ${ITERS:-30} 2>/dev/null | sed "s/^{/{\"variant\": \"$v\", \"round\": $r, /" >> gpurun_out/ab.jsonl
+    PICO_LIB_PATH=picotron_amd/lib/variants/$v.so timeout -k 10 120 python scripts/attn_bench.py --configs ${ATTN_CONFIGS:-c2} --iters ${ITERS:-30} 2>/dev/null | sed "s/^{/{\"variant\": \"$v\", \"round\": $r, /" >> gpurun_out/ab.jsonl
     rc=${PIPESTATUS[0]}
     if [ "$rc" -ne 0 ]; then echo "variant $v failed rc=$rc"; exit $rc; fi
   done

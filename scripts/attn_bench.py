@@ -47,7 +47,7 @@ def main():
             o, lse = ops.attention_block_fwd(q, k, v, sc, causal)
             ops.attention_block_bwd(do, q, k, v, o, lse, sc, causal)
         torch.cuda.synchronize()
-        ids = [L.K_ATTN_FWD, L.K_ATTN_BWD_PRE, L.K_ATTN_BWD, L.K_ATTN_BWD_DQ, L.K_ATTN_BWD_DKV, L.K_ATTN_BWD_Q,
+        ids = [L.K_ATTN_FWD, L.K_ATTN_BWD_DKV, L.K_ATTN_BWD_Q,
                L.K_ATTN_BWD_KV]
         for i in ids:
             L.prof_enable(i, args.iters + 4)

@@ -41,7 +41,6 @@ def main(iters=100):
     o_t = torch.empty(H * D, B * S, dtype=torch.bfloat16, device="cuda")
     res = {
         "lib": os.path.basename(os.environ.get("PICO_LIB_PATH", "shipped")),
-        "fwd64": os.environ.get("PICO_ATTN_FWD64", "0"),
         "fwd_us": timed(lambda: ops.attention_block_fwd(q, k, v, sc, True), iters, L.K_ATTN_FWD),
         "fwd_rope_q_us": timed(lambda: ops.attention_block_fwd(q, k, v, sc, True, rope_q=(cos, sin)), iters, L.K_ATTN_FWD),
         "fwd_step_us": timed(lambda: ops.attention_block_fwd(q, k, v, sc, True, o_t=o_t, rope_q=(cos, sin)), iters, L.K_ATTN_FWD),

@@ -110,14 +110,16 @@ def test_ops_fail_loudly_without_hip_tensors(lib):
 
 def test_weight_transpose_cache_host_logic(monkeypatch):
     """ops.weight_t's cache: one entry per weight storage, reused across the fresh stacked views each call
-    builds; safe by default — writes through `.data` (no version bump), in-place writes
-    through the parameter (version bump), `.data` rebinds and optimizer steps all make the next use
-    re-transpose, with no explicit invalidate_weight_transposes(); entries hold their parameters only weakly
+    builds. In-place writes through the parameter (version counter), `.data` rebinds (storage key),
+    load_state_dict and optimizer steps (step post-hook) make the next use re-transpose by themselves; reading
+    `.data` does not (no torch class is patched: VERDICT r03 item 6); a write through a `.data`
+    alias is the documented case for invalidate_weight_transposes(). Entries hold their parameters only weakly
     and die with them. (CPU tensors: the transpose falls back to a strided copy; the cache logic is the same.)"""
     import gc
     from picotron_amd import ops
     monkeypatch.setattr(ops, "_WT_CACHE", {})
     monkeypatch.setattr(ops, "_WT_HOOK", [])
+    assert not isinstance(torch.nn.Parameter.__dict__.get("data"), property)  # torch itself is left alone
     a = torch.nn.Parameter(torch.randn(8, 16))
     b = torch.nn.Parameter(torch.randn(8, 16))
 
@@ -127,12 +129,19 @@ def test_weight_transpose_cache_host_logic(monkeypatch):
     t1 = ops.weight_t(ops.stacked_weight((a, b)), (a, b))
     assert torch.equal(t1, torch.cat([a, b]).t())
     assert ops.weight_t(ops.stacked_weight((a, b)), (a, b)) is t1 and len(ops._WT_CACHE) == 1
-    gen = ops._WT_GEN[0]
+    gen, n0 = ops._WT_GEN[0], ops._WT_STATS["transposes"]
     assert ops.weight_t(ops.stacked_weight((a, b)), (a, b)) is t1 and ops._WT_GEN[0] == gen  # no spurious bumps
+    # reads of .data (logging, weight norms, EMA, deepcopy) neither bump the generation nor re-transpose
+    _ = float(a.data.norm()) + float(b.data.abs().max())
+    import copy
+    copy.deepcopy(a)
+    assert ops._WT_GEN[0] == gen
+    assert ops.weight_t(ops.stacked_weight((a, b)), (a, b)) is t1 and ops._WT_STATS["transposes"] == n0
     with torch.no_grad():
-        a.data.mul_(2)  # bumps no version counter: seen through the watched .data property
+        a.data.mul_(2)  # a `.data` alias has its own version counter: the documented explicit invalidation
+    ops.invalidate_weight_transposes()
     assert fresh()
-    b.data.copy_(torch.randn(8, 16))
+    a.data = torch.randn(8, 16)  # rebind: new storage
     assert fresh()
     with torch.no_grad():
         a.add_(1.0)  # version counter
@@ -163,3 +172,26 @@ def test_build_tracks_included_sources():
     deps = B.deps(d128)
     assert os.path.join(B.CSRC, "attn_bwd_split.hip") in deps
     assert os.path.abspath(B.__file__) in deps
+
+
+def test_flash_atten_0_is_refused(monkeypatch):
+    """The reference's FLASH_ATTEN switch (ref picotron/model.py:126,151,191,247): this package has no eager path,
+    so FLASH_ATTEN=0 raises a clear error at model construction (where the reference picks its RMSNorm class) and
+    in Attention.forward, instead of silently running the kernels."""
+    from picotron_amd import model as M
+    cfg = M.LlamaConfig(hidden_size=64, intermediate_size=128, num_attention_heads=2, num_key_value_heads=2,
+                        num_hidden_layers=1, vocab_size=64, max_position_embeddings=16)
+    monkeypatch.delenv("FLASH_ATTEN", raising=False)
+    with torch.device("meta"):
+        m = M.Llama(cfg)  # default (unset) and "1": the kernel path
+    monkeypatch.setenv("FLASH_ATTEN", "1")
+    with torch.device("meta"):
+        M.Llama(cfg)
+    monkeypatch.setenv("FLASH_ATTEN", "0")
+    for build in (lambda: M.Llama(cfg), lambda: M.DecoderLayer(cfg, 0)):
+        with pytest.raises(RuntimeError, match="FLASH_ATTEN"):
+            with torch.device("meta"):
+                build()
+    x = torch.empty(1, 4, 64, device="meta")
+    with pytest.raises(RuntimeError, match="FLASH_ATTEN"):
+        m.decoder_layers[0].attention(x, None, None)

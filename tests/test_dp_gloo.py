@@ -190,3 +190,61 @@ def test_fused_ready_with_persistent_grads(tmp_path):
             got = torch.load(tmp_path / f"s{step}_r{r}.pt", weights_only=True)
             assert torch.allclose(got["a"], torch.full((4,), sa)), (step, r, got["a"])
             assert torch.allclose(got["b"], torch.full((4,), sb)), (step, r, got["b"])
+
+
+def _defer_worker(rank, world, port, outdir):
+    """DataParallelBucket(defer_grad_cast=True) under a torch.optim optimizer: the deferred fp32 ->
+    .grad cast is run by the bucket's global step pre-hook before torch.optim.AdamW steps, so the step equals the
+    eager-cast run's bit for bit; only picotron_amd.optim.AdamW (which reads main_grad itself) skips it."""
+    import sys
+    sys.path.insert(0, ROOT)
+    torch.set_num_threads(1)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from safetensors.torch import load_file
+    from oracle import hotpath as H
+    from oracle import model as OM
+    from picotron_amd import process_group_manager as pgm
+    from picotron_amd.data import synth_tokens
+    from picotron_amd.data_parallel import bucket as B
+    from picotron_amd.data_parallel.data_parallel import DataParallelBucket
+    pgm.setup_process_group_manager(tp_size=1, cp_size=1, pp_size=1, dp_size=world)
+    B.set_kernels(H.CpuBucketKernels())
+    cfg = SimpleNamespace(**TINY_DP)
+    gold = load_file(os.path.join(GOLDEN, "dp_w2_tiny.safetensors"))
+    init = {k[5:]: v for k, v in gold.items() if k.startswith("init.")}
+    res = {}
+    for defer in (False, True):
+        model = OM.Llama(cfg)
+        model.load_state_dict(init, strict=True)
+        ddp = DataParallelBucket(model, bucket_cap_mb=0.05, defer_grad_cast=defer)
+        for go in ddp.bucket_manager.grad_out_list:
+            go.fill_(float("nan"))  # what an unrun cast would leave visible
+        opt = torch.optim.AdamW(model.parameters(), lr=1e-2)
+        gen = torch.Generator().manual_seed(5 + rank)
+        for step in range(2):
+            opt.zero_grad(set_to_none=False)
+            for i in range(2):
+                toks = synth_tokens(2, cfg.max_position_embeddings + 1, cfg.vocab_size, gen, "arith")
+                ddp.require_backward_grad_sync = i == 1
+                logits = ddp(input_ids=toks[:, :-1])
+                loss = torch.nn.functional.cross_entropy(logits.reshape(-1, cfg.vocab_size), toks[:, 1:].reshape(-1))
+                (loss / 2).backward()
+            opt.step()
+            for p in model.parameters():
+                assert torch.equal(p.grad, p.main_grad), "the optimizer stepped on an un-cast .grad"
+                assert not getattr(p, "_pico_grad_deferred", False)
+            ddp.reset()
+        res[defer] = {n: p.detach().clone() for n, p in model.named_parameters()}
+    for n in res[False]:
+        assert torch.equal(res[False][n], res[True][n]), n
+    torch.save({"ok": True}, os.path.join(outdir, f"defer_r{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def test_deferred_cast_materialized_for_torch_optimizers(tmp_path):
+    world = 2
+    mp.start_processes(_defer_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    for r in range(world):
+        assert torch.load(tmp_path / f"defer_r{r}.pt", weights_only=True)["ok"]

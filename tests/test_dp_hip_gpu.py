@@ -11,6 +11,7 @@ the bucket all-reduce and the bf16 cast on the side stream — over grad_acc = 3
   * PICO_WGRAD_FUSION flipped between micro-batches (fused -> plain -> fused): no micro-batch may be
     dropped (the sticky per-param flag of round 1 could drop one).
 """
+import math
 import os
 import socket
 
@@ -193,3 +194,134 @@ def test_adamw_reads_deferred_fp32_grads_bit_exact(tmp_path):
         for name in c:
             for a, b in zip(c[name], d[name]):
                 assert torch.equal(a, b), name
+
+
+# ------------------------------------------------------------------------------------------------------------
+# C3 at its workload: SmolLM-1.7B geometry, DP = 8, the bench's own step
+# ------------------------------------------------------------------------------------------------------------
+C3_GA = 2
+C3_LAYERS = 2
+
+
+def _c3_head(model):
+    """A non-zero LM head (the reference init zeroes it, ref picotron/checkpoint.py:88-91, which would leave every
+    gradient below the head zero at step 0): the same values in every process."""
+    with torch.no_grad():
+        g = torch.Generator().manual_seed(7)
+        w = model.final_proj.weight
+        w.copy_((torch.randn(w.shape, generator=g) * 0.02).to(w.dtype))
+
+
+def _c3_ref_worker(rank, world, port, out_path):
+    """One process, W = 1: the eight ranks' micro-batches (each rank's SyntheticDataLoader stream) accumulated
+    eagerly into fp32 main_grad — the sum the all-reduced buckets must equal 8x of."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1")
+    import sys
+    import torch.distributed as dist
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    import bench
+    from picotron_amd import process_group_manager as pgm
+    from picotron_amd.data import SyntheticDataLoader
+    from picotron_amd.data_parallel.data_parallel import DataParallelBucket
+    from picotron_amd.train import _micro_batch
+    pgm.setup_process_group_manager(tp_size=1, cp_size=1, pp_size=1, dp_size=1)
+    dev = torch.device("cuda", 0)
+    cfg, model, _, _, _ = bench.setup(C3_LAYERS, C3_GA, 1, dev, "pico", True, post_build=_c3_head)
+    model = DataParallelBucket(model)
+    batches = []
+    for r in range(8):
+        ld = SyntheticDataLoader(bench.MBS, bench.SEQ, C3_GA, cfg.vocab_size, seed=1234, kind="uniform",
+                                 num_batches=C3_GA, device=dev, dp_rank=r)
+        batches += [next(ld) for _ in range(C3_GA)]
+    for i, b in enumerate(batches):
+        model.require_backward_grad_sync = i == len(batches) - 1
+        _micro_batch(model, b["input_ids"], b["target_ids"], C3_GA)
+    torch.cuda.synchronize()
+    torch.save([g.cpu() for g in model.bucket_manager.grad_data_list], out_path)
+    dist.destroy_process_group()
+
+
+def _c3_worker(rank, world, port, ref_path, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import hashlib
+    import sys
+    import torch.distributed as dist
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    from picotron_amd import process_group_manager as pgm
+    from picotron_amd.optim import AdamW
+    from picotron_amd.train import TrainingStep
+    pgm.setup_process_group_manager(tp_size=1, cp_size=1, pp_size=1, dp_size=world)
+    dev = torch.device("cuda", 0)
+    # exactly bench.py --gpus 8's objects and step (DataParallelBucket(defer_grad_cast=True), pico AdamW, graphs)
+    cfg, model, opt, loader, _ = bench.setup(C3_LAYERS, C3_GA, world, dev, "pico", True, post_build=_c3_head)
+    step = TrainingStep(model, opt, loader, dev, graphs=True)
+    res = {"rank": rank, "buckets": len(model.bucket_manager.buckets),
+           "bucket_mb": [round(g.numel() * 4 / 2**20, 1) for g in model.bucket_manager.grad_data_list]}
+    step.zero()
+    loss = step.micro_batches(sync_loss=True)  # micro-batch 0 from the graph, 1 eager + bucket all-reduces
+    torch.cuda.synchronize()
+    res["loss"] = loss
+    res["replayed"] = step.graphs.graph is not None
+    # (1) every bucket == 1/8 of the one-process fp32 sum (fp32 summation order only)
+    ref = torch.load(ref_path, weights_only=True)
+    errs = []
+    for g, gr in zip(model.bucket_manager.grad_data_list, ref):
+        r = gr.to(dev) / world
+        errs.append(float((g - r).double().norm() / r.double().norm().clamp_min(1e-30)))
+    res["bucket_rel_err"] = errs
+    h = hashlib.sha1()
+    for g in model.bucket_manager.grad_data_list:
+        h.update(g.cpu().numpy())
+    res["sha"] = h.hexdigest()
+    params = list(model.module.parameters())
+    res["deferred"] = all(getattr(p, "_pico_grad_deferred", False) for p in params)
+    # (2) AdamW on the deferred fp32 main_grad == cast-then-step, bit for bit (params and both moments)
+    shadow = [torch.nn.Parameter(p.detach().clone()) for p in params]
+    for s_, p in zip(shadow, params):
+        s_.grad = p.main_grad.to(torch.bfloat16)
+    ref_opt = AdamW(shadow, lr=3e-4)
+    ref_opt.step()
+    step.optimizer_step()
+    torch.cuda.synchronize()
+    res["adam_equal"] = all(torch.equal(p, s_) and torch.equal(opt.state[p]["exp_avg"], ref_opt.state[s_]["exp_avg"])
+                            and torch.equal(opt.state[p]["exp_avg_sq"], ref_opt.state[s_]["exp_avg_sq"])
+                            for p, s_ in zip(params, shadow))
+    # (3) the deferred cast, when asked for, writes exactly the bf16 .grad of the eager path
+    model.materialize_grads()
+    res["grad_equal"] = all(torch.equal(p.grad, p.main_grad.to(torch.bfloat16)) for p in params)
+    step.reset()
+    torch.save(res, os.path.join(out_dir, f"c3_r{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+def test_c3_smollm_dp8_bench_step(tmp_path):
+    """C3 (SmolLM-1.7B DP = 8, ref picotron/data_parallel/bucket.py:25-31,84-129, data_parallel.py:122-165) at its
+    real bucket layout: eight gloo ranks share this GPU (RCCL refuses several ranks on one device) and run
+    bench.py's own setup and TrainingStep — SmolLM-1.7B geometry with 2 layers (so the 402 MB embedding and LM-head
+    buckets are present), micro-batch 4, seq 1024, grad_acc 2 (one graph replay + the syncing eager micro-batch),
+    DataParallelBucket(defer_grad_cast=True) and the pico AdamW. Checks: every bucket equals 1/8 of a one-process
+    fp32 sum over the eight ranks' micro-batches (rel-L2 <= 4e-6: summation order only), the eight replicas are
+    bit-identical, AdamW on the deferred fp32 main_grad equals cast-then-step bit for bit, and the materialised
+    .grad equals the bf16 cast bit for bit."""
+    ref_path = str(tmp_path / "c3_ref.pt")
+    mp.start_processes(_c3_ref_worker, args=(1, _free_port(), ref_path), nprocs=1, join=True, start_method="spawn")
+    world = 8
+    mp.start_processes(_c3_worker, args=(world, _free_port(), ref_path, str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    res = [torch.load(tmp_path / f"c3_r{r}.pt", weights_only=True) for r in range(world)]
+    r0 = res[0]
+    assert r0["buckets"] == 17  # embedding, 2 x (q + 2 norms, k, v, out, up, gate, down), final_proj, final_norm
+    assert max(r0["bucket_mb"]) > 380  # the 402 MB embedding / LM-head buckets
+    for r in res:
+        assert r["replayed"] and r["deferred"], r["rank"]
+        assert max(r["bucket_rel_err"]) <= 4e-6, (r["rank"], max(r["bucket_rel_err"]))
+        assert r["sha"] == r0["sha"], r["rank"]  # identical replicas
+        assert r["adam_equal"] and r["grad_equal"], r["rank"]
+        assert math.isfinite(r["loss"])

@@ -353,6 +353,39 @@ def test_wt_dgrad_tracks_weights(golden_loss, monkeypatch):
             assert rel_l2(res["1"][i][n].cpu(), res["0"][i][n].cpu()) < 2e-2, (i, n)
 
 
+def test_wt_refresh_once_per_weight_per_step(golden_loss):
+    """a reference-shaped loop (zero_grad, 2 micro-batches, a per-step `.data` read for
+    logging, optimizer.step()) re-transposes every cached W^T exactly once per optimizer step — reads of `.data` do
+    not invalidate the cache (no torch class is patched), the step post-hook does."""
+    from picotron_amd import ops
+    from picotron_amd.model import build_llama
+    from picotron_amd.optim import AdamW
+    from picotron_amd.train import _micro_batch
+    cfg = _cfg(golden_loss)
+    torch.manual_seed(7)
+    m = build_llama(cfg, "cuda", BF)
+    with torch.no_grad():
+        m.final_proj.weight.normal_(0, 0.02, generator=torch.Generator("cuda").manual_seed(1))
+    opt = AdamW(m.parameters(), lr=1e-3)
+    g = torch.Generator("cuda").manual_seed(3)
+    counts = []
+    for step in range(6):
+        opt.zero_grad()
+        n0 = ops._WT_STATS["transposes"]
+        for _ in range(2):
+            t = torch.randint(0, cfg.vocab_size, (2, 129), device="cuda", generator=g)
+            _micro_batch(m, t[:, :-1], t[:, 1:], 2)
+        norms = [float(p.data.norm()) for p in m.parameters()]  # logging-style reads of .data
+        assert all(math.isfinite(x) for x in norms)
+        opt.step()
+        counts.append(ops._WT_STATS["transposes"] - n0)
+    ops._wt_purge()
+    mine = {id(p) for p in m.parameters()}
+    live = sum(1 for e in ops._WT_CACHE.values() if all(r() is not None and id(r()) in mine for r in e[2]))
+    assert live > 0
+    assert counts[1:] == [live] * 5, (counts, live)  # steady state: one per cached weight per optimizer step
+
+
 def test_graph_replay_matches_eager(golden_loss):
     """MicroBatchGraph (HIP-graph replay of forward + CE + backward) gives the eager loop's loss and
     gradients bit for bit over a 3-micro-batch step, and a second step after an optimizer update."""
@@ -445,17 +478,18 @@ def test_graph_replay_with_dp_bucket(golden_loss):
 
 def test_bench_dp2_gloo_on_one_gpu():
     """The N > 1 bench path end to end (DataParallelBucket + graph-replayed micro-batches + bucket
-    all-reduce + busbw measurement) with two ranks sharing this GPU. RCCL refuses two ranks on one
-    device, so the rehearsal uses the gloo backend; the 8-GPU RCCL run is the driver's."""
+    all-reduce + busbw measurement) with two ranks sharing this GPU, started as `python bench.py --gpus 2` WITHOUT a
+    launcher: bench.py spawns its own torch.distributed.run job before touching the GPU, and
+    rank 0 prints the one JSON line. RCCL refuses two ranks on one device, so the rehearsal uses the gloo backend;
+    the 8-GPU RCCL run is the driver's."""
     import json
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="4")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(root, "bench.py"),
-           "--gpus", "2", "--backend", "gloo", "--layers", "2", "--grad-acc", "3", "--steps", "2", "--warmup", "1",
-           "--no-cpu-baseline"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="4")
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--backend", "gloo", "--layers", "2",
+           "--grad-acc", "3", "--steps", "2", "--warmup", "1", "--no-cpu-baseline"]
     p = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stderr[-3000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
