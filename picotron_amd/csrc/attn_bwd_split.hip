@@ -479,20 +479,24 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kv_kernel(const pico_
   // per-lane byte offsets of this wave's pieces within a full tile (computed once; partial tiles clamp)
   unsigned pc_off[C::NPW];
 #pragma unroll
-  for (int i = 0; i < C::NPW; ++i) {
-    if (pc_kind[i] == 2) pc_off[i] = (unsigned)pc_row[i] * 4u + (pc_col[i] ? delta_off : 0u);
-    else pc_off[i] = (unsigned)(pc_row[i] * (pc_kind[i] == 0 ? qs1 : ds1) + pc_col[i] * 2);
-  }
+  for (int i = 0; i < C::NP / KNW; ++i) pc_off[i] = (unsigned)(pc_row[i] * (pc_kind[i] == 0 ? qs1 : ds1) + pc_col[i] * 2);
   const bool ragged = Sq % QT != 0;
   auto issue = [&](int si, const Tc& c) __attribute__((always_inline)) {
     const unsigned dst = ring_lds + (unsigned)si * (unsigned)C::SLOT;
 #pragma unroll
     for (int i = 0; i < C::NPW; ++i) {
-      if (i < C::NP / KNW || wave < C::NP % KNW) {
+      if (i < C::NP / KNW) {
         unsigned off = pc_off[i];
         if (ragged && c.q0 + QT > Sq && pc_kind[i] != 2)  // partial tile: clamp rows past Sq - 1
           off = (unsigned)((min(c.q0 + pc_row[i], Sq - 1) - c.q0) * (pc_kind[i] == 0 ? qs1 : ds1) + pc_col[i] * 2);
         dma_piece(c.p[i], off, dst + pc_dst[i]);
+      } else if (wave < C::NP % KNW) {
+        // the tile's LSE / delta piece (wave 0 only, pc_kind 2): its per-lane offset is re-derived from the lane
+        // id here instead of being held in a VGPR for the whole sweep — at 168 VGPRs that VGPR was spilled, and
+        // its scratch reload's vmcnt(0) drained wave 0's whole DMA queue (two tiles of prefetch) every tile
+        static_assert(C::NP % KNW == 1 && C::NP / KNW == C::NPW - 1, "the LSE / delta piece is wave 0's last");
+        const int l = (int)__lane_id() & 15;
+        dma_piece(c.p[i], (unsigned)(16 * (l & 7)) + ((l >> 3) ? delta_off : 0u), dst + pc_dst[i]);
       }
     }
   };
@@ -809,7 +813,7 @@ int launch_split(const pico_attn_args* a, hipStream_t s) {
   if constexpr (D == 128) {
     PICO_TRY(pico_launch(PICO_K_ATTN_BWD_KV, "attn_bwd_kv", attn_bwd_kv_kernel<D, CAUSAL, 1>, dim3((int)nblk),
                          dim3(KNW * 64), 0, s, *a, a->softmax_scale, sl2, lse2, delta, sq_pad, hsplit, dkv_part, stamps));
-  } else if (CAUSAL) {
+  } else if constexpr (CAUSAL) {
     PICO_TRY(pico_launch(PICO_K_ATTN_BWD_KV, "attn_bwd_kv", attn_bwd_kv_kernel<D, CAUSAL, 3>, dim3((int)nblk),
                          dim3(KNW * 64), 0, s, *a, a->softmax_scale, sl2, lse2, delta, sq_pad, hsplit, dkv_part, stamps));
   } else {

@@ -240,6 +240,7 @@ def _c3_ref_worker(rank, world, port, out_path):
         _micro_batch(model, b["input_ids"], b["target_ids"], C3_GA)
     torch.cuda.synchronize()
     torch.save([g.cpu() for g in model.bucket_manager.grad_data_list], out_path)
+    print("[c3 ref] one-process sum over 8 x 2 micro-batches saved", file=sys.stderr, flush=True)
     dist.destroy_process_group()
 
 
@@ -262,8 +263,10 @@ def _c3_worker(rank, world, port, ref_path, out_dir):
     step = TrainingStep(model, opt, loader, dev, graphs=True)
     res = {"rank": rank, "buckets": len(model.bucket_manager.buckets),
            "bucket_mb": [round(g.numel() * 4 / 2**20, 1) for g in model.bucket_manager.grad_data_list]}
+    print(f"[c3 rank {rank}] model built, {res['buckets']} buckets", file=sys.stderr, flush=True)
     step.zero()
     loss = step.micro_batches(sync_loss=True)  # micro-batch 0 from the graph, 1 eager + bucket all-reduces
+    print(f"[c3 rank {rank}] micro-batches done, loss {loss:.4f}", file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     res["loss"] = loss
     res["replayed"] = step.graphs.graph is not None

@@ -121,6 +121,43 @@ def test_rmsnorm_chained_dw(monkeypatch, rows, cols):
         assert rel_l2(a, r) < 1e-2
 
 
+@pytest.mark.parametrize("reentrant", [False, True])
+def test_rmsnorm_chained_dw_under_checkpoint(reentrant):
+    """a norm forward that runs INSIDE a backward pass (activation recompute by
+    torch.utils.checkpoint) must not drop the chained weight gradient another norm of that pass left pending.
+    Three stacked norms with persistent .grad (chained dw), the middle one checkpointed: weight gradients equal
+    the run without checkpointing."""
+    from torch.utils.checkpoint import checkpoint
+    ops = _ops()
+    torch.manual_seed(11)
+    rows, cols = 512, 2048
+    x0 = torch.randn(rows, cols, dtype=BF, device=DEV) * 2
+    ws = [(1 + 0.1 * torch.randn(cols, device=DEV)).to(BF) for _ in range(3)]
+    dy = torch.randn(rows, cols, dtype=BF, device=DEV)
+
+    def run(ckpt):
+        params = [w.clone().requires_grad_(True) for w in ws]
+        for p in params:
+            p.grad = torch.zeros_like(p)
+        x = x0.clone().requires_grad_(True)
+        h = ops.rms_norm(x, params[0], 1e-5)
+        if ckpt:
+            h = checkpoint(lambda t: ops.rms_norm(t, params[1], 1e-5), h, use_reentrant=reentrant)
+        else:
+            h = ops.rms_norm(h, params[1], 1e-5)
+        h = ops.rms_norm(h, params[2], 1e-5)
+        h.backward(dy)
+        torch.cuda.synchronize()
+        assert not ops._NORM_PENDING
+        return [p.grad.float().cpu() for p in params], x.grad.float().cpu()
+
+    g_ref, dx_ref = run(False)
+    g_ck, dx_ck = run(True)
+    assert torch.equal(dx_ck, dx_ref)
+    for a, b in zip(g_ck, g_ref):
+        assert max_abs(a, b) <= _ulp_bound(b.double(), 1), max_abs(a, b)
+
+
 def test_rmsnorm_residual_prenorm():
     ops = _ops()
     torch.manual_seed(1)
