@@ -213,24 +213,38 @@ __attribute__((amdgpu_waves_per_eu(FwdCfg<D>::WAVES_PER_EU, FwdCfg<D>::WAVES_PER
     }
   }
   // element offsets within a tile for full tiles (rows never clamped)
-  unsigned src_off[C::NIW];
+  unsigned src_off_b[C::NIW];
 #pragma unroll
-  for (int i = 0; i < C::NIW; ++i) src_off[i] = (unsigned)(src_row[i] * (is_k[i] ? ksd : vsd) + src_col[i]);
+  for (int i = 0; i < C::NIW; ++i) src_off_b[i] = (unsigned)(src_row[i] * (is_k[i] ? ksd : vsd) + src_col[i]) * 2u;
+  const char* const kbase = (const char*)kg;
+  const char* const vbase = (const char*)vg;
+  const int64_t kst = (int64_t)BN * ksd * 2, vst = (int64_t)BN * vsd * 2;  // bytes per tile
+  const unsigned smem_lds0 = (unsigned)__builtin_amdgcn_readfirstlane((int)lds_addr(smem));
   auto issue = [&](int tile) __attribute__((always_inline)) {
     char* slot = smem + (unsigned)(tile % C::NBUF) * (unsigned)C::SLOT;
     const int base = tile * BN;
     if (base + BN <= Sk) {
+      const unsigned sl = smem_lds0 + (unsigned)(tile % C::NBUF) * (unsigned)C::SLOT;
+#pragma unroll
+      for (int i = 0; i < C::NIW; ++i)
+        dma_piece(is_k[i] ? kbase + tile * kst : vbase + tile * vst, src_off_b[i], sl + dst_off[i]);
+    } else {  // last, partial tile
+      int ln;
+      asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
 #pragma unroll
       for (int i = 0; i < C::NIW; ++i) {
-        const bf16_t* tb = is_k[i] ? kg + (int64_t)base * ksd : vg + (int64_t)base * vsd;
-        __builtin_amdgcn_global_load_lds((const void*)(tb + src_off[i]),
-                                         (__attribute__((address_space(3))) void*)(slot + dst_off[i]), 16, 0, 0);
-      }
-    } else {  // last, partial tile: clamp rows (finite values; the softmax masks keys >= Sk)
-#pragma unroll
-      for (int i = 0; i < C::NIW; ++i) {
-        const int key = min(base + src_row[i], Sk - 1);
-        const bf16_t* src = is_k[i] ? kg + (int64_t)key * ksd + src_col[i] : vg + (int64_t)key * vsd + src_col[i];
+        const int j = wave + 4 * i;
+        int row, col;
+        if (j < 2 * KS) {
+          row = 32 * (j & 1) + (ln >> 1);
+          col = 16 * (j >> 1) + 8 * ((ln & 1) ^ ((row >> 3) & 1));
+        } else {
+          const int jv = j - 2 * KS;
+          row = 16 * (jv & 3) + (ln >> 2);
+          col = 32 * (jv >> 2) + 8 * (ln & 3);
+        }
+        const int key = min(base + row, Sk - 1);
+        const bf16_t* src = is_k[i] ? kg + (int64_t)key * ksd + col : vg + (int64_t)key * vsd + col;
         __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(slot + dst_off[i]),
                                          16, 0, 0);
       }
@@ -245,7 +259,8 @@ __attribute__((amdgpu_waves_per_eu(FwdCfg<D>::WAVES_PER_EU, FwdCfg<D>::WAVES_PER
   f32x16 o[DT];
 #pragma unroll
   for (int dt = 0; dt < DT; ++dt) o[dt] = (f32x16)0.f;
-  float m_i = -INFINITY;  // running max of scale*log2e*s (scaled domain)
+  float m_i = -INFINITY, neg_m = 0.f, thr_raw = -INFINITY;
+  const float inv_sl2 = 1.f / scale_log2;
   float l_i = 0.f;        // per-lane partial row sum (this lane's keys only)
 
   // V^T operands for keys 32 kt .. 32 kt + 31 of the tile (2 st x DT, inline-asm transposed reads)
@@ -315,17 +330,17 @@ __attribute__((amdgpu_waves_per_eu(FwdCfg<D>::WAVES_PER_EU, FwdCfg<D>::WAVES_PER
     for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
       for (int i = (kt == 0 ? 1 : 0); i < 16; ++i) mx = fmaxf(mx, s[kt][i]);
-    const float m_tile = halves_max(mx) * scale_log2;
-    // rescale only when some row's max grew (wave-uniform); exact
-    if (__builtin_amdgcn_ballot_w64(m_tile > m_i + (float)PICO_FWD_RESCALE_THR)) {
+    if (__builtin_amdgcn_ballot_w64(mx > thr_raw)) {
+      const float m_tile = halves_max(mx) * scale_log2;
       const float m_new = fmaxf(m_i, m_tile);
       const float alpha = m_i == -INFINITY ? 0.f : fast_exp2(m_i - m_new);
       l_i *= alpha;
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) o[dt] *= alpha;
       m_i = m_new;
+      neg_m = m_i == -INFINITY ? 0.f : -m_i;
+      thr_raw = (m_i + (float)PICO_FWD_RESCALE_THR) * inv_sl2;
     }
-    const float neg_m = m_i == -INFINITY ? 0.f : -m_i;
     float lsum0 = 0.f, lsum1 = 0.f;
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt)
@@ -379,23 +394,29 @@ __attribute__((amdgpu_waves_per_eu(FwdCfg<D>::WAVES_PER_EU, FwdCfg<D>::WAVES_PER
   wgs[1] = __builtin_amdgcn_s_memrealtime();
   __builtin_amdgcn_s_waitcnt(0xC07F);
 #endif
-  for (int t = 0; t < ntiles; ++t) {
-    // tile t's pieces landed (this wave's), then every wave's (barrier); later tiles stay in flight
-    if (P == 2 && t + 1 < ntiles) {
-      if constexpr (C::NIW == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();
-    // slot (t + P) % NBUF was last read in iteration t - 1, which every wave has finished
-    if (t + P < ntiles) issue(t + P);
-    const int n0 = t * BN;
-    // wave-uniform: skip (tile above every row), full (every key visible to every row), or masked
-    if (n0 <= lim_last) {
-      const unsigned slot = (unsigned)(t % C::NBUF) * (unsigned)C::SLOT;
-      const char* kb = smem + (slot + k_lane);
-      tile_body(kb, smem_lds + slot + v_lane, n0, n0 + BN - 1 > lim_first);
+  // unrolled by the ring depth: every ring slot is a compile-time offset in the LDS reads
+  for (int t0 = 0; t0 < ntiles; t0 += C::NBUF) {
+#pragma unroll
+    for (int u = 0; u < C::NBUF; ++u) {
+      const int t = t0 + u;
+      if (t >= ntiles) break;
+      // tile t's pieces landed (this wave's), then every wave's (barrier); later tiles stay in flight
+      if (P == 2 && t + 1 < ntiles) {
+        if constexpr (C::NIW == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __builtin_amdgcn_s_barrier();
+      // slot (t + P) % NBUF was last read in iteration t - 1, which every wave has finished
+      if (t + P < ntiles) issue(t + P);
+      const int n0 = t * BN;
+      // wave-uniform: skip (tile above every row), full (every key visible to every row), or masked
+      if (n0 <= lim_last) {
+        const unsigned slot = (unsigned)u * (unsigned)C::SLOT;
+        const char* kb = smem + (slot + k_lane);
+        tile_body(kb, smem_lds + slot + v_lane, n0, n0 + BN - 1 > lim_first);
+      }
     }
   }
 

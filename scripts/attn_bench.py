@@ -75,8 +75,6 @@ def main():
                 tot_bwd += us
         L.load().pico_prof_enable(0, 0)
         res["fwd_tflops"] = round(fl / (res["attn_fwd_us"] * 1e-6) / 1e12, 1)
-        main = res["attn_bwd_us"] or res["attn_bwd_kv_us"]
-        res["bwd_kernel_tflops"] = round(2.5 * fl / (main * 1e-6) / 1e12, 1) if main else None
         res["bwd_total_tflops"] = round(2.5 * fl / (tot_bwd * 1e-6) / 1e12, 1)
         res["bwd_wall_tflops"] = round(2.5 * fl / (res["bwd_wall_us"] * 1e-6) / 1e12, 1)
         res["fwd_bwd_tflops"] = round(3.5 * fl / ((res["attn_fwd_us"] + tot_bwd) * 1e-6) / 1e12, 1)

@@ -21,6 +21,8 @@ CASES = {  # B, S, Hq, Hkv, D, causal
     "gqa4": (4, 1024, 32, 8, 64, True),
     "s4096": (1, 4096, 32, 32, 64, True),
     "full": (2, 1024, 8, 8, 64, False),
+    "fold5": (6, 640, 32, 32, 64, True),      # 5 blocks x 192 heads > one round: one folded pair per head
+    "fold_ragged": (7, 1000, 32, 32, 64, True),  # ragged last block inside a folded pair
     "d128": (2, 1024, 16, 16, 128, True),   # Llama-2-7B per tp-2 rank
     "d128_ragged": (1, 1000, 8, 8, 128, True),
     "d128_full": (2, 1024, 16, 16, 128, False),
