@@ -65,10 +65,14 @@ class _RMSNormFn(torch.autograd.Function):
             res_out = torch.empty_like(x2)
         w = weight.contiguous()
         yt = None
+        t_only = False
         if want_t and os.getenv("PICO_XT_WGRAD", "1") != "0" and cols in (1024, 2048) and rows % 32 == 0 and \
                 all(t is None or t.data_ptr() % 16 == 0 for t in (x2, res2, w)):
             # y^T as a by-product for the next projection's TT wgrad GEMM (no separate transpose pass)
             yt = torch.empty((cols, rows), dtype=x.dtype, device=x.device)
+            t_only = act_t_only()
+            if t_only:  # the consumers read y as the transposed view of y^T: y itself is never written
+                y = None
             _lib.check(lib.pico_rmsnorm_fwd_t(_lib.ptr(x2), _lib.ptr(res2), _lib.ptr(w), _lib.ptr(y), _lib.ptr(res_out),
                                               _lib.ptr(rstd), _lib.ptr(yt), rows, rows, cols, float(eps),
                                               _lib.stream_of(x)), "pico_rmsnorm_fwd_t")
@@ -82,7 +86,7 @@ class _RMSNormFn(torch.autograd.Function):
         ctx.shape = shape
         ctx.has_residual = residual is not None
         ctx.prenorm = prenorm
-        y = y.view(shape)
+        y = (yt.t() if t_only else y).view(shape)
         if yt is not None:
             y._pico_t = yt
         if prenorm:
@@ -463,6 +467,13 @@ def transpose_2d(x, out=None):
     return out
 
 
+def act_t_only():
+    """PICO_ACT_T_ONLY=1: the RMSNorm (y^T form) and SwiGLU (h^T form) producers write ONLY the transposed
+    activation; the next projection's forward GEMM reads it through the transposed view (hipBLASLt's
+    transposed-A form), saving the row-major write (16.8 MB per norm, 67 MB per SwiGLU at C2)."""
+    return os.getenv("PICO_ACT_T_ONLY", "0") == "1"
+
+
 def _wgrad_input(x2, n_out, x=None):
     """What the backward keeps of a projection's input x2 [T, K] for its wgrad: x2 itself, or x2^T as a
     transposed view of a contiguous [K, T] copy where hipBLASLt's "TT" wgrad form saves more than the
@@ -506,18 +517,39 @@ def _conc_tags():
 
 
 _SIDE = {}
+_NO_SIDE = [0]  # > 0: the dgrad / wgrad (and LM-head dx / dW) pairs run in sequence on the caller's stream
+
+
+@contextlib.contextmanager
+def no_side_streams():
+    """Within: no side-stream fork / join in dgrad_wgrad or the chunked LM-head CE (the pipelined micro-batch
+    graph, whose two micro-batches already share the chip: a fork from its forked slot stream, i.e. dependencies
+    in both directions between two non-origin capture streams, crashes hipStreamEndCapture on this ROCm)."""
+    _NO_SIDE[0] += 1
+    try:
+        yield
+    finally:
+        _NO_SIDE[0] -= 1
+
+
+def _side_stream(dev):
+    """The side stream paired with the caller's current stream on `dev` (one per (device, stream): the two
+    streams of the pipelined micro-batches each fork to their own, so neither waits on the other's work)."""
+    key = (dev, torch.cuda.current_stream(dev).cuda_stream)
+    side = _SIDE.get(key)
+    if side is None:
+        side = _SIDE[key] = torch.cuda.Stream(device=dev)
+    return side
 
 
 def dgrad_wgrad(tag, dy2, W, params, x2):
     """(dx, wgrad_accumulate(...)) for one projection; concurrently on two streams when `tag` is enabled
     (joined before returning: everything after the projection's backward sees both results). Joining later
     (the next projection's backward) measured the same: the fork / join edges cost ≈ 6 + 11 µs either way."""
-    if tag in _conc_tags() and dy2.is_cuda:
+    if tag in _conc_tags() and dy2.is_cuda and not _NO_SIDE[0]:
         dev = dy2.device
         cur = torch.cuda.current_stream(dev)
-        side = _SIDE.get(dev)
-        if side is None:
-            side = _SIDE[dev] = torch.cuda.Stream(device=dev)
+        side = _side_stream(dev)
         side.wait_stream(cur)
         with torch.cuda.stream(side):
             dws = wgrad_accumulate(params, dy2, x2)
@@ -774,7 +806,7 @@ class _LMHeadCEChunkedFn(torch.autograd.Function):
                 elif g.is_contiguous() and g.dtype == w.dtype and tuple(g.shape) == tuple(w.shape):
                     kind, dst = "grad", g
         lib = _lib.load()
-        conc = "lm" in _conc_tags()
+        conc = "lm" in _conc_tags() and not _NO_SIDE[0]
         for c0 in range(0, T, chunk):
             c1 = min(T, c0 + chunk)
             n = c1 - c0
@@ -788,9 +820,7 @@ class _LMHeadCEChunkedFn(torch.autograd.Function):
             # before the next chunk overwrites the logits buffer)
             side = None
             if conc and need_w:
-                side = _SIDE.get(x.device)
-                if side is None:
-                    side = _SIDE[x.device] = torch.cuda.Stream(device=x.device)
+                side = _side_stream(x.device)
                 side.wait_stream(torch.cuda.current_stream(x.device))
             if need_w:
                 xc = xin[c0:c1]
@@ -948,15 +978,19 @@ class _GateUpSwiGLUFn(torch.autograd.Function):
         x2 = x.reshape(-1, x.shape[-1])
         gu = torch.matmul(x2, W.t())  # [T, 2I]
         T = gu.shape[0]
-        h = torch.empty((T, I), dtype=x.dtype, device=x.device)
         ht = None
         if os.getenv("PICO_XT_WGRAD", "1") != "0" and os.getenv("PICO_SWIGLU_T", "1") != "0" and T % 64 == 0 \
                 and I % 64 == 0 and gu.data_ptr() % 16 == 0:
-            # h^T as a by-product (the down projection's wgrad reads it in the TT GEMM form)
+            # h^T as a by-product (the down projection's wgrad reads it in the TT GEMM form); with act_t_only()
+            # h is the transposed view of h^T and never written
             ht = torch.empty((I, T), dtype=x.dtype, device=x.device)
-            _lib.check(_lib.load().pico_swiglu_fwd_t(_lib.ptr(gu), _lib.ptr(gu[:, I:]), _lib.ptr(h), _lib.ptr(ht), T, I,
-                                                     2 * I, I, T, _lib.stream_of(gu)), "pico_swiglu_fwd_t")
+            h = ht.t() if act_t_only() else torch.empty((T, I), dtype=x.dtype, device=x.device)
+            _lib.check(_lib.load().pico_swiglu_fwd_t(_lib.ptr(gu), _lib.ptr(gu[:, I:]),
+                                                     None if h.data_ptr() == ht.data_ptr() else _lib.ptr(h),
+                                                     _lib.ptr(ht), T, I, 2 * I, I, T, _lib.stream_of(gu)),
+                       "pico_swiglu_fwd_t")
         else:
+            h = torch.empty((T, I), dtype=x.dtype, device=x.device)
             _swiglu_fwd(gu, gu[:, I:], h, T, I, 2 * I, I)
         ctx.save_for_backward(_wgrad_input(x2, 2 * I, x), gu, W)
         ctx.params = (w_gate, w_up)

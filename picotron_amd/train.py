@@ -38,9 +38,9 @@ def _fused_lm_head(model):
     return head
 
 
-def _micro_batch(model, input_ids, target_ids, grad_acc_steps, loss_acc=None):
-    """One micro-batch forward + backward (ref train.py:39-51); returns the detached loss. loss_acc (fp32 device
-    scalar): += the loss — inside the fused CE's mean launch when the chunked form runs, else one add."""
+def _forward_loss(model, input_ids, target_ids, grad_acc_steps, loss_acc=None):
+    """One micro-batch forward to its mean CE / grad_acc (ref train.py:39-49): (loss, folded). folded: the loss
+    was already added into loss_acc (fp32 device scalar) by the fused CE's mean launch (the chunked form)."""
     head = _fused_lm_head(model)
     folded = False
     if head is not None:  # fused LM head + cross-entropy (SURVEY §8f row 1): logits never re-read
@@ -57,6 +57,13 @@ def _micro_batch(model, input_ids, target_ids, grad_acc_steps, loss_acc=None):
         batch_size, seq_len = input_ids.shape
         outputs = outputs.view(seq_len * batch_size, -1)
         loss = _cross_entropy(outputs, target_ids.reshape(-1)) / grad_acc_steps
+    return loss, folded
+
+
+def _micro_batch(model, input_ids, target_ids, grad_acc_steps, loss_acc=None):
+    """One micro-batch forward + backward (ref train.py:39-51); returns the detached loss. loss_acc (fp32 device
+    scalar): += the loss — inside the fused CE's mean launch when the chunked form runs, else one add."""
+    loss, folded = _forward_loss(model, input_ids, target_ids, grad_acc_steps, loss_acc)
     loss.backward()
     if loss_acc is not None and not folded:
         loss_acc += loss.detach()
@@ -75,17 +82,32 @@ def train_step(model, data_loader, device, graphs=None, sync_loss=True):
     requires_grad_sync = (m is not None and m.cp_dp_world_size > 1) or hasattr(model, "require_backward_grad_sync")
     losses = []
     n = data_loader.grad_acc_steps
+    grouped = graphs is not None and getattr(graphs, "grouped", False)
+    pending = []  # grouped graphs: the non-syncing micro-batches, replayed together before the syncing one
+
+    def run_pending():
+        if pending:
+            if requires_grad_sync:
+                model.require_backward_grad_sync = False
+            graphs.run(pending)
+            pending.clear()
+
     for i in range(n):
         batch = next(data_loader)
         input_ids = batch["input_ids"].to(device)
         target_ids = batch["target_ids"].to(device)
         sync = requires_grad_sync and i == n - 1
+        if grouped and not sync:
+            pending.append((input_ids, target_ids))
+            continue
+        run_pending()
         if requires_grad_sync:
             model.require_backward_grad_sync = sync
         if graphs is not None and not sync:  # syncing micro-batches launch RCCL from hooks: eager
             graphs.replay(input_ids, target_ids)
         else:
             losses.append(_micro_batch(model, input_ids, target_ids, n))
+    run_pending()
     if graphs is not None:
         losses.append(graphs.take_loss())
     # one host sync per step instead of one per micro-batch (ref :53 calls .item() each time), or none
@@ -155,6 +177,118 @@ class MicroBatchGraph:
         return out
 
 
+class PipelinedMicroBatchGraph:
+    """The non-syncing micro-batches of a step captured as ONE HIP graph, software-pipelined over two streams:
+    the forward of micro-batch i runs beside the backward of micro-batch i - 1, so the GEMMs that cannot fill
+    the chip alone (the 2048-wide out / down projections: 128 tiles of 256 x 256 for 256 CUs) and the HBM-bound
+    kernels share it with the other micro-batch's work. Results are those of the serial loop bit for bit: the
+    backwards stay in micro-batch order (backward i waits for backward i - 1, so every gradient accumulates in
+    the same order) and so do the forwards (forward i waits for forward i - 1: the chunked LM-head CE adds its
+    weight gradient and the loss in the forward). Same contract as MicroBatchGraph (persistent gradient
+    buffers zeroed in place; capture at the start of a step), one replay per step instead of one per
+    micro-batch; `train_step` hands it the step's non-syncing micro-batches together (`run`)."""
+
+    grouped = True
+
+    def __init__(self, model, grad_acc_steps, zero_grads):
+        self.model = model
+        self.n = grad_acc_steps
+        self.zero_grads = zero_grads
+        self.graphs = {}  # number of micro-batches -> (graph, inputs [k, B, S], targets [k, B, S])
+        self.loss_acc = None
+        self.streams = None
+
+    @property
+    def graph(self):
+        return next(iter(self.graphs.values()))[0] if self.graphs else None
+
+    def _body(self, inp, tgt):
+        from . import ops
+        with ops.no_side_streams():
+            self._pipeline(inp, tgt)
+
+    def _pipeline(self, inp, tgt):
+        model, n, acc = self.model, self.n, self.loss_acc
+        cur = torch.cuda.current_stream()
+        # slot 0 runs on the capture stream itself, slot 1 on one stream forked from it: with BOTH slots on
+        # forked streams (dependencies in both directions between two forked streams) hipStreamEndCapture
+        # segfaults on this ROCm (scripts/dbg_event_capture.py reproduces it with plain tensor ops)
+        streams = (cur, self.streams[1])
+        streams[1].wait_stream(cur)
+        k = inp.shape[0]
+        losses = [None] * k
+        bwd_done = fwd_done = None
+        for i in range(k + 1):
+            if i >= 1:  # backward of micro-batch i - 1 (on its forward's stream), after backward i - 2
+                st = streams[(i - 1) % 2]
+                with torch.cuda.stream(st):
+                    if bwd_done is not None:
+                        st.wait_event(bwd_done)
+                    loss, folded = losses[i - 1]
+                    loss.backward()
+                    if not folded:
+                        acc += loss.detach()
+                    bwd_done = torch.cuda.Event()
+                    bwd_done.record(st)
+                losses[i - 1] = None
+            if i < k:  # forward of micro-batch i, after forward i - 1
+                st = streams[i % 2]
+                with torch.cuda.stream(st):
+                    if fwd_done is not None:
+                        st.wait_event(fwd_done)
+                    losses[i] = _forward_loss(model, inp[i], tgt[i], n, acc)
+                    fwd_done = torch.cuda.Event()
+                    fwd_done.record(st)
+        cur.wait_stream(streams[1])
+
+    def _capture(self, batches):
+        dev = batches[0][0].device
+        if self.streams is None:
+            self.streams = (None, torch.cuda.Stream(device=dev))  # slot 0: the caller's (capture) stream
+        inp = torch.stack([b[0] for b in batches])
+        tgt = torch.stack([b[1] for b in batches])
+        if self.loss_acc is None:
+            self.loss_acc = torch.zeros((), dtype=torch.float32, device=dev)
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(1 if len(batches) > 1 else 2):  # eager warm-up: at least two micro-batches
+                self._body(inp, tgt)
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._body(inp, tgt)
+        torch.cuda.synchronize()
+        self.zero_grads()
+        self.loss_acc.zero_()
+        self.graphs[len(batches)] = (g, inp, tgt)
+
+    def run(self, batches):
+        from . import ops
+        ops.refresh_weight_transposes()  # dgrad W^T copies are graph inputs: bring them up to date
+        if len(batches) not in self.graphs:
+            self._capture(batches)
+        g, inp, tgt = self.graphs[len(batches)]
+        for j, (x, y) in enumerate(batches):
+            inp[j].copy_(x)
+            tgt[j].copy_(y)
+        g.replay()
+
+    def take_loss(self):
+        if self.loss_acc is None:
+            return torch.zeros(())
+        out = self.loss_acc.clone()
+        self.loss_acc.zero_()
+        return out
+
+
+def pipelined_enabled():
+    """PICO_MB_PIPELINE=1: TrainingStep's graphs replay the step's micro-batches as one two-stream pipelined
+    graph (PipelinedMicroBatchGraph); 0: one MicroBatchGraph replay per micro-batch."""
+    return os.getenv("PICO_MB_PIPELINE", "0") == "1"
+
+
 class TrainingStep:
     """One optimizer step of the reference loop (ref train.py:219-240) on this hot path, exactly as bench.py runs
     it: optimizer.zero_grad(), train_step over grad_acc micro-batches (the non-syncing ones replayed from a HIP
@@ -167,7 +301,8 @@ class TrainingStep:
         self.optimizer = optimizer
         self.loader = loader
         self.device = device
-        self.graphs = MicroBatchGraph(model, loader.grad_acc_steps, self.zero_grads) if graphs else None
+        cls = PipelinedMicroBatchGraph if pipelined_enabled() else MicroBatchGraph
+        self.graphs = cls(model, loader.grad_acc_steps, self.zero_grads) if graphs else None
 
     def zero_grads(self):
         """Zero every gradient buffer in place (graph replays keep persistent buffers)."""

@@ -57,8 +57,8 @@ def main():
         torch.cuda.synchronize()
         fl = 4.0 * B * Hq * S * S * D * (0.5 if causal else 1.0)
         res = {"config": name, "B": B, "S": S, "Hq": Hq, "Hkv": Hkv, "D": D, "causal": causal}
-        # wall time of the whole backward call on the caller's stream (kernel timers off): with the
-        # concurrent split form (PICO_ATTN_CONC=1) the sum of kernel times overstates it
+        # wall time of the whole backward call on the caller's stream (kernel timers off): the dQ and dK/dV
+        # kernels plus the launch gaps between them
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(args.iters):

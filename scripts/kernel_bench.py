@@ -2,7 +2,14 @@
 hidden 2048, intermediate 8192, 32 + 32 heads of 64): RMSNorm fwd/bwd (residual form), RoPE (q|k in
 place on the fused qkv buffer), SwiGLU fwd/bwd (strided halves of the gate|up buffer), embedding
 bwd. Times each launch with the library's HIP-event timer; prints one JSON line per kernel with
-algorithmic GB/s (every input read once + every output written once)."""
+algorithmic GB/s (every input read once + every output written once).
+
+  python scripts/kernel_bench.py [--cold] [--iters 50]
+
+--cold writes a 1 GiB buffer between launches (untimed: the kernel timer brackets the kernel alone), so
+every launch reads its inputs from HBM instead of the 256 MB MALL / L2 that a back-to-back loop leaves them
+in — the condition the kernels meet inside the training step, where the GEMMs between them evict everything."""
+import argparse
 import json
 import os
 import sys
@@ -12,7 +19,12 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def main(iters=50):
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--cold", action="store_true")
+    args = ap.parse_args()
+    iters = args.iters
     from picotron_amd import _lib as L
     from picotron_amd import ops
     L.load()
@@ -85,6 +97,7 @@ def main(iters=50):
         ("transpose_x", lambda: ops.transpose_2d(x.detach(), out=xt), [L.K_TRANSPOSE]),
         ("transpose_wgu", lambda: ops.transpose_2d(wgu, out=wgut), [L.K_TRANSPOSE]),
     ]
+    flush = torch.empty(1 << 29, dtype=torch.bfloat16, device=dev) if args.cold else None
     work = {L.K_RMSNORM_FWD: 4 * T * H * 2 + 4 * T, L.K_RMSNORM_BWD: 4 * T * H * 2 + 4 * T,
             L.K_ROPE: 2 * T * 2 * NH * D * 2, L.K_SWIGLU_FWD: 3 * T * I * 2, L.K_SWIGLU_BWD: 5 * T * I * 2,
             L.K_EMBEDDING_BWD: T * H * 2 + 2 * T * H * 2, L.K_CE_FWD: 2 * T * V * 2}
@@ -94,18 +107,22 @@ def main(iters=50):
             work[L.K_TRANSPOSE] = tbytes[name]
         work[L.K_SWIGLU_FWD] = (4 if name == "swiglu_t" else 3) * T * I * 2
         work[L.K_ROPE] = 2 * T * (1 if name == "rope_k" else 2) * NH * D * 2
+        # the y^T form also writes y^T (x, r read; residual, y, y^T written)
+        work[L.K_RMSNORM_FWD] = (5 if name == "rmsnorm_t" else 4) * T * H * 2 + 4 * T
         for _ in range(3):
             fn()
         torch.cuda.synchronize()
         for k in kids:
             L.prof_enable(k, iters + 8)
         for _ in range(iters):
+            if flush is not None:
+                flush.fill_(1.0)
             fn()
         torch.cuda.synchronize()
         for k in kids:
             ms, n = L.prof_collect(k)
             us = 1e3 * ms / max(n, 1)
-            out = {"kernel": L.KERNEL_NAMES[k] + ("" if k not in (L.K_TRANSPOSE,) and name not in ("rmsnorm_t", "swiglu_t", "rmsnorm_chain", "rope_k") else ":" + name), "avg_us": round(us, 2), "launches": n}
+            out = {"cold": bool(args.cold), "kernel": L.KERNEL_NAMES[k] + ("" if k not in (L.K_TRANSPOSE,) and name not in ("rmsnorm_t", "swiglu_t", "rmsnorm_chain", "rope_k") else ":" + name), "avg_us": round(us, 2), "launches": n}
             if k in work:
                 out["GB_s"] = round(work[k] / (us * 1e-6) / 1e9, 1)
                 out["frac_of_8TBs"] = round(out["GB_s"] / 8000, 3)

@@ -1,7 +1,10 @@
 """Probe: how much does overlapping micro-batch i+1's forward with micro-batch i's backward (two HIP streams)
 gain over the serial grad-accumulation loop (ref train.py:33-51), eagerly, at the C2 shape?
 
-  python scripts/overlap_probe.py [--layers 15] [--n 16] [--reps 3]
+  python scripts/overlap_probe.py [--layers 15] [--n 16] [--reps 3] [--graph]
+
+--graph captures each order once as a HIP graph and times its replays (the bench's form: eagerly the host
+issue rate, not the device, bounds a micro-batch).
 
 Serial: fwd(i), bwd(i) for i in 0..n-1 on one stream. Overlapped: fwd(i) on stream i % 2; bwd(i - 1) is issued
 before fwd(i) and runs on its forward's stream (autograd); bwd(i) waits for bwd(i - 1) (the gradient buffers
@@ -24,6 +27,7 @@ def main():
     ap.add_argument("--layers", type=int, default=15)
     ap.add_argument("--n", type=int, default=16)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--graph", action="store_true")
     args = ap.parse_args()
     from picotron_amd import _lib, ops
     from picotron_amd.model import build_llama, smollm_1_7b
@@ -84,11 +88,29 @@ def main():
         for st in s:
             main.wait_stream(st)
 
+    def graphed(body):
+        ops.refresh_weight_transposes()
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            body()
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            body()
+        torch.cuda.synchronize()
+        return g.replay
+
     res = {}
     grads = {}
     params = list(model.parameters())
     check = params[:8] + params[-2:]
-    for name, fn in (("serial", serial), ("overlap", overlapped), ("serial2", serial), ("overlap2", overlapped)):
+    orders = {"serial": serial, "overlap": overlapped}
+    if args.graph:
+        orders = {k: graphed(v) for k, v in orders.items()}
+    for name, fn in (("serial", orders["serial"]), ("overlap", orders["overlap"]), ("serial2", orders["serial"]),
+                     ("overlap2", orders["overlap"])):
         zero()
         fn()  # warm-up (and the gradients of one pass, for the comparison)
         torch.cuda.synchronize()
@@ -103,7 +125,8 @@ def main():
             ts.append(time.perf_counter() - t0)
         res[name] = round(1e3 * min(ts) / n, 3)
     diff = max(float((a - b).abs().max()) for a, b in zip(grads["serial"], grads["overlap"]))
-    print(json.dumps({"ms_per_microbatch": res, "max_grad_diff": diff, "layers": args.layers, "n": n}), flush=True)
+    print(json.dumps({"ms_per_microbatch": res, "max_grad_diff": diff, "layers": args.layers, "n": n,
+                      "graph": args.graph}), flush=True)
 
 
 if __name__ == "__main__":

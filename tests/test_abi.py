@@ -195,3 +195,43 @@ def test_flash_atten_0_is_refused(monkeypatch):
     x = torch.empty(1, 4, 64, device="meta")
     with pytest.raises(RuntimeError, match="FLASH_ATTEN"):
         m.decoder_layers[0].attention(x, None, None)
+
+
+def test_train_step_groups_non_syncing_micro_batches():
+    """train_step with a grouped graph object (PipelinedMicroBatchGraph's interface): the non-syncing
+    micro-batches are handed over together, in loader order and with the DP sync flag off, BEFORE the syncing
+    micro-batch runs eagerly with the flag on (host logic; a CPU stand-in model and graph object)."""
+    from picotron_amd.data import SyntheticDataLoader
+    from picotron_amd.train import train_step
+
+    class Tiny(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.emb = torch.nn.Embedding(64, 8)
+            self.out = torch.nn.Linear(8, 64, bias=False)
+            self.require_backward_grad_sync = True
+            self.log = []
+
+        def forward(self, input_ids):
+            self.log.append(("eager", self.require_backward_grad_sync, input_ids[0, 0].item()))
+            return self.out(self.emb(input_ids))
+
+    class Grouped:
+        grouped = True
+
+        def __init__(self, model):
+            self.model = model
+
+        def run(self, batches):
+            self.model.log.append(("group", self.model.require_backward_grad_sync,
+                                   [b[0][0, 0].item() for b in batches]))
+
+        def take_loss(self):
+            return torch.zeros(())
+
+    m = Tiny()
+    loader = SyntheticDataLoader(2, 16, 4, 64, seed=3, num_batches=4)
+    firsts = [next(loader)["input_ids"][0, 0].item() for _ in range(4)]
+    loader = SyntheticDataLoader(2, 16, 4, 64, seed=3, num_batches=4)
+    train_step(m, loader, "cpu", graphs=Grouped(m))
+    assert m.log == [("group", False, firsts[:3]), ("eager", True, firsts[3])], m.log

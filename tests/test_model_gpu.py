@@ -240,6 +240,33 @@ def test_micro_batch_fused_lm_head_ce(golden_loss, monkeypatch, chunk):
         assert rel_l2(outs["1"][1][n].cpu(), outs["0"][1][n].cpu()) < 3e-2, n
 
 
+def test_act_t_only_matches(monkeypatch):
+    """PICO_ACT_T_ONLY=1 (the RMSNorm and SwiGLU producers write only y^T / h^T; the next projections read the
+    transposed views) == the default form: loss and every gradient of two micro-batches (hidden 1024, so the norm's
+    y^T form runs), within bf16 tolerance (the GEMMs' transposed-A kernels may tile differently)."""
+    from picotron_amd import ops, train
+    from picotron_amd.model import LlamaConfig, build_llama
+    from conftest import rel_l2
+    cfg = LlamaConfig(hidden_size=1024, intermediate_size=2048, num_attention_heads=16, num_key_value_heads=16,
+                      num_hidden_layers=2, vocab_size=512, max_position_embeddings=128)
+    g = torch.Generator("cuda").manual_seed(17)
+    toks = [torch.randint(0, cfg.vocab_size, (2, 129), device="cuda", generator=g) for _ in range(2)]
+    outs = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("PICO_ACT_T_ONLY", mode)
+        assert ops.act_t_only() == (mode == "1")
+        torch.manual_seed(7)
+        m = build_llama(cfg, "cuda", BF)
+        with torch.no_grad():
+            m.final_proj.weight.normal_(0, 0.02, generator=torch.Generator("cuda").manual_seed(1))
+        losses = [train._micro_batch(m, t[:, :-1], t[:, 1:], 2) for t in toks]
+        torch.cuda.synchronize()
+        outs[mode] = (sum(float(l) for l in losses), {n: p.grad.float().clone() for n, p in m.named_parameters()})
+    assert abs(outs["1"][0] - outs["0"][0]) <= 1e-3 * abs(outs["0"][0]), (outs["0"][0], outs["1"][0])
+    for n in outs["0"][1]:
+        assert rel_l2(outs["1"][1][n].cpu(), outs["0"][1][n].cpu()) < 1e-2, n
+
+
 def _train_grads(cfg, toks, fusion, monkeypatch, dp=None):
     """grad_acc = len(toks) micro-batches; returns {name: fp32 grad (or main_grad with DP)}."""
     from picotron_amd.model import build_llama
@@ -386,12 +413,15 @@ def test_wt_refresh_once_per_weight_per_step(golden_loss):
     assert counts[1:] == [live] * 5, (counts, live)  # steady state: one per cached weight per optimizer step
 
 
-def test_graph_replay_matches_eager(golden_loss):
-    """MicroBatchGraph (HIP-graph replay of forward + CE + backward) gives the eager loop's loss and
-    gradients bit for bit over a 3-micro-batch step, and a second step after an optimizer update."""
+@pytest.mark.parametrize("kind", ["per_micro_batch", "pipelined"])
+def test_graph_replay_matches_eager(golden_loss, kind):
+    """MicroBatchGraph (HIP-graph replay of forward + CE + backward) — or PipelinedMicroBatchGraph (the step's
+    micro-batches as one graph, forward i beside backward i - 1 on two streams) — gives the eager loop's loss
+    and gradients bit for bit over a 3-micro-batch step, and a second step after an optimizer update."""
     from picotron_amd.data import SyntheticDataLoader
     from picotron_amd.model import build_llama
-    from picotron_amd.train import MicroBatchGraph, train_step
+    from picotron_amd.train import MicroBatchGraph, PipelinedMicroBatchGraph, train_step
+    cls = PipelinedMicroBatchGraph if kind == "pipelined" else MicroBatchGraph
     cfg = _cfg(golden_loss)
     results = []
     for use_graph in (False, True):
@@ -406,7 +436,7 @@ def test_graph_replay_matches_eager(golden_loss):
             for p in m.parameters():
                 if p.grad is not None:
                     p.grad.zero_()
-        g = MicroBatchGraph(m, 3, zero) if use_graph else None
+        g = cls(m, 3, zero) if use_graph else None
         losses, grads = [], None
         for step in range(2):
             opt.zero_grad(set_to_none=False)
@@ -423,16 +453,18 @@ def test_graph_replay_matches_eager(golden_loss):
         assert torch.equal(p0[n], p1[n]), n
 
 
-def test_graph_replay_with_dp_bucket(golden_loss):
-    """DataParallelBucket (RCCL, W = 1) + MicroBatchGraph: the non-syncing micro-batches replay as a
-    graph (their DP hooks' accumulates are captured), the syncing one runs eagerly; main_grad, .grad
-    and the updated parameters equal the all-eager loop bit for bit, over two steps."""
+@pytest.mark.parametrize("kind", ["per_micro_batch", "pipelined"])
+def test_graph_replay_with_dp_bucket(golden_loss, kind):
+    """DataParallelBucket (RCCL, W = 1) + MicroBatchGraph (or PipelinedMicroBatchGraph): the non-syncing
+    micro-batches replay as a graph (their DP hooks' accumulates are captured), the syncing one runs eagerly;
+    main_grad, .grad and the updated parameters equal the all-eager loop bit for bit, over two steps."""
     import torch.distributed as dist
     from picotron_amd import process_group_manager as pgm
     from picotron_amd.data import SyntheticDataLoader
     from picotron_amd.data_parallel.data_parallel import DataParallelBucket
     from picotron_amd.model import build_llama
-    from picotron_amd.train import MicroBatchGraph, train_step
+    from picotron_amd.train import MicroBatchGraph, PipelinedMicroBatchGraph, train_step
+    cls = PipelinedMicroBatchGraph if kind == "pipelined" else MicroBatchGraph
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0", WORLD_SIZE="1",
                       LOCAL_RANK="0")
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
@@ -454,7 +486,7 @@ def test_graph_replay_with_dp_bucket(golden_loss):
                     if p.grad is not None:
                         p.grad.zero_()
                 ddp.bucket_manager.reset()
-            g = MicroBatchGraph(ddp, 3, zero) if use_graph else None
+            g = cls(ddp, 3, zero) if use_graph else None
             losses, snap = [], None
             for step in range(2):
                 opt.zero_grad(set_to_none=not use_graph)
