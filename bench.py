@@ -193,7 +193,7 @@ def main():
 
     from picotron_amd import _lib as L
     from picotron_amd import process_group_manager as pgm
-    from picotron_amd.train import TrainingStep, get_mfu, train_step
+    from picotron_amd.train import TrainingStep, get_mfu, pipelined_enabled, train_step
 
     L.load()
     pgm.setup_process_group_manager(tp_size=1, cp_size=1, pp_size=1, dp_size=world)
@@ -339,7 +339,10 @@ def main():
                                        args.grad_acc, " pico_adamw_bf16" if args.optimizer == "pico" else
                                        (" torch fused" if args.fused_adam else " torch")),
                        "model": "SmolLM-1.7B-%dL" % args.layers, "global_batch": MBS * args.grad_acc * world,
-                       "seq_len": SEQ, "micro_batch": MBS, "grad_acc": args.grad_acc, "parallelism": f"dp{world}"},
+                       "seq_len": SEQ, "micro_batch": MBS, "grad_acc": args.grad_acc, "parallelism": f"dp{world}",
+                       "schedule": ("eager" if not args.graphs else
+                                    "pipelined graph (forward i beside backward i-1)" if pipelined_enabled() else
+                                    "graph per micro-batch")},
             "tokens_per_sec_per_gpu": round(tps_gpu, 1),
             "mfu_pct": round(mfu, 2),
             "mfu_peak_tflops": round(BF16_PEAK_TFLOPS, 1),

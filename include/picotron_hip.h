@@ -91,8 +91,7 @@ int pico_prof_collect(int kernel_id, double* total_ms, int64_t* launches);
  * for backward). residual (optional, may be NULL): x_eff = bf16(x + residual), written to
  * residual_out when residual_out != NULL (layer_norm_fn(prenorm=True) semantics). */
 /* pico_rmsnorm_fwd that also writes y^T ([cols, rows], row stride ld_t): the x^T the next projection's
- * weight-gradient GEMM reads. cols 1024 or 2048, rows multiple of 32, 16-byte aligned pointers. y may be
- * NULL: only y^T is written (consumers that read y through its transposed view). */
+ * weight-gradient GEMM reads. cols 1024 or 2048, rows multiple of 32, 16-byte aligned pointers. */
 int pico_rmsnorm_fwd_t(const void* x, const void* residual, const void* weight, void* y, void* residual_out,
                        float* rstd, void* y_t, int64_t ld_t, int64_t rows, int64_t cols, float eps, void* stream);
 int pico_rmsnorm_fwd(const void* x, const void* residual, const void* weight, void* y,
@@ -143,8 +142,7 @@ int pico_rope(const void* x, void* out, const void* cos, const void* sin, int64_
  * gate/up (and dgate/dup) rows at element stride in_stride (they may be the two column halves of one
  * fused gate|up GEMM output, in_stride = 2*cols); out/dout rows at out_stride. */
 /* pico_swiglu_fwd that also writes out^T ([cols, rows], row stride t_stride): the down projection's
- * x^T for its weight-gradient GEMM. rows, cols multiples of 64; strides multiples of 8. out may be NULL:
- * only out^T is written (the down projection then reads h through the transposed view). */
+ * x^T for its weight-gradient GEMM. rows, cols multiples of 64; strides multiples of 8. */
 int pico_swiglu_fwd_t(const void* gate, const void* up, void* out, void* out_t, int64_t rows, int64_t cols,
                       int64_t in_stride, int64_t out_stride, int64_t t_stride, void* stream);
 int pico_swiglu_fwd(const void* gate, const void* up, void* out, int64_t rows, int64_t cols,

@@ -167,7 +167,7 @@ __global__ __launch_bounds__(FWDT_WAVES * 64) void rmsnorm_fwd_t_kernel(const bf
       u16x8 o;
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = f2bf(bf2f(xr[k][c][j]) * rs * wf[j]);
-      if (y) *reinterpret_cast<u16x8*>(y + row * COLS + col) = o;  // null: the consumers read y^T only
+      *reinterpret_cast<u16x8*>(y + row * COLS + col) = o;
       *reinterpret_cast<u16x8*>(tile + lr * PITCH + col) = o;
     }
   }
@@ -428,7 +428,7 @@ extern "C" {
 
 int pico_rmsnorm_fwd_t(const void* x, const void* residual, const void* weight, void* y, void* residual_out,
                        float* rstd, void* y_t, int64_t ld_t, int64_t rows, int64_t cols, float eps, void* stream) {
-  PICO_REQUIRE(x && weight && rstd && y_t, "pico_rmsnorm_fwd_t: null pointer");  // y may be null (y^T only)
+  PICO_REQUIRE(x && weight && y && rstd && y_t, "pico_rmsnorm_fwd_t: null pointer");
   PICO_REQUIRE(cols == 1024 || cols == 2048, "pico_rmsnorm_fwd_t: cols=%lld unsupported (1024 or 2048)",
                (long long)cols);
   PICO_REQUIRE(rows >= 0 && rows % 32 == 0 && ld_t >= rows && ld_t % 8 == 0,

@@ -99,7 +99,7 @@ __global__ __launch_bounds__(TC * 4) void swiglu_fwd_t_kernel(const bf16_t* __re
       const float gf = bf2f(gv[j]);
       o[j] = f2bf(gf * sigmoidf_(gf) * bf2f(uv[j]));
     }
-    if (h) *reinterpret_cast<u16x8*>(h + row * os + c0 + lc) = o;  // null: the consumer reads h^T only
+    *reinterpret_cast<u16x8*>(h + row * os + c0 + lc) = o;
     unsigned* d = reinterpret_cast<unsigned*>(tile + (lr + 32 * p) * TP + lc);
 #pragma unroll
     for (int k = 0; k < 4; ++k) d[k] = (unsigned)o[2 * k] | ((unsigned)o[2 * k + 1] << 16);
@@ -161,7 +161,7 @@ extern "C" {
 
 int pico_swiglu_fwd_t(const void* gate, const void* up, void* out, void* out_t, int64_t rows, int64_t cols,
                       int64_t in_stride, int64_t out_stride, int64_t t_stride, void* stream) {
-  PICO_REQUIRE(gate && up && out_t, "pico_swiglu_fwd_t: null pointer");  // out may be null (h^T only)
+  PICO_REQUIRE(gate && up && out && out_t, "pico_swiglu_fwd_t: null pointer");
   PICO_REQUIRE(rows >= 0 && cols >= 0 && rows % 64 == 0 && cols % 64 == 0,
                "pico_swiglu_fwd_t: rows and cols must be multiples of 64");
   PICO_REQUIRE(in_stride >= cols && out_stride >= cols && t_stride >= rows && in_stride % 8 == 0 &&

@@ -65,14 +65,10 @@ class _RMSNormFn(torch.autograd.Function):
             res_out = torch.empty_like(x2)
         w = weight.contiguous()
         yt = None
-        t_only = False
         if want_t and os.getenv("PICO_XT_WGRAD", "1") != "0" and cols in (1024, 2048) and rows % 32 == 0 and \
                 all(t is None or t.data_ptr() % 16 == 0 for t in (x2, res2, w)):
             # y^T as a by-product for the next projection's TT wgrad GEMM (no separate transpose pass)
             yt = torch.empty((cols, rows), dtype=x.dtype, device=x.device)
-            t_only = act_t_only()
-            if t_only:  # the consumers read y as the transposed view of y^T: y itself is never written
-                y = None
             _lib.check(lib.pico_rmsnorm_fwd_t(_lib.ptr(x2), _lib.ptr(res2), _lib.ptr(w), _lib.ptr(y), _lib.ptr(res_out),
                                               _lib.ptr(rstd), _lib.ptr(yt), rows, rows, cols, float(eps),
                                               _lib.stream_of(x)), "pico_rmsnorm_fwd_t")
@@ -86,7 +82,7 @@ class _RMSNormFn(torch.autograd.Function):
         ctx.shape = shape
         ctx.has_residual = residual is not None
         ctx.prenorm = prenorm
-        y = (yt.t() if t_only else y).view(shape)
+        y = y.view(shape)
         if yt is not None:
             y._pico_t = yt
         if prenorm:
@@ -465,13 +461,6 @@ def transpose_2d(x, out=None):
     _lib.check(_lib.load().pico_transpose_bf16(_lib.ptr(x), x.stride(0), _lib.ptr(out), out.stride(0), R, C,
                                                _lib.stream_of(x)), "pico_transpose_bf16")
     return out
-
-
-def act_t_only():
-    """PICO_ACT_T_ONLY=1: the RMSNorm (y^T form) and SwiGLU (h^T form) producers write ONLY the transposed
-    activation; the next projection's forward GEMM reads it through the transposed view (hipBLASLt's
-    transposed-A form), saving the row-major write (16.8 MB per norm, 67 MB per SwiGLU at C2)."""
-    return os.getenv("PICO_ACT_T_ONLY", "0") == "1"
 
 
 def _wgrad_input(x2, n_out, x=None):
@@ -978,19 +967,15 @@ class _GateUpSwiGLUFn(torch.autograd.Function):
         x2 = x.reshape(-1, x.shape[-1])
         gu = torch.matmul(x2, W.t())  # [T, 2I]
         T = gu.shape[0]
+        h = torch.empty((T, I), dtype=x.dtype, device=x.device)
         ht = None
         if os.getenv("PICO_XT_WGRAD", "1") != "0" and os.getenv("PICO_SWIGLU_T", "1") != "0" and T % 64 == 0 \
                 and I % 64 == 0 and gu.data_ptr() % 16 == 0:
-            # h^T as a by-product (the down projection's wgrad reads it in the TT GEMM form); with act_t_only()
-            # h is the transposed view of h^T and never written
+            # h^T as a by-product (the down projection's wgrad reads it in the TT GEMM form)
             ht = torch.empty((I, T), dtype=x.dtype, device=x.device)
-            h = ht.t() if act_t_only() else torch.empty((T, I), dtype=x.dtype, device=x.device)
-            _lib.check(_lib.load().pico_swiglu_fwd_t(_lib.ptr(gu), _lib.ptr(gu[:, I:]),
-                                                     None if h.data_ptr() == ht.data_ptr() else _lib.ptr(h),
-                                                     _lib.ptr(ht), T, I, 2 * I, I, T, _lib.stream_of(gu)),
-                       "pico_swiglu_fwd_t")
+            _lib.check(_lib.load().pico_swiglu_fwd_t(_lib.ptr(gu), _lib.ptr(gu[:, I:]), _lib.ptr(h), _lib.ptr(ht), T, I,
+                                                     2 * I, I, T, _lib.stream_of(gu)), "pico_swiglu_fwd_t")
         else:
-            h = torch.empty((T, I), dtype=x.dtype, device=x.device)
             _swiglu_fwd(gu, gu[:, I:], h, T, I, 2 * I, I)
         ctx.save_for_backward(_wgrad_input(x2, 2 * I, x), gu, W)
         ctx.params = (w_gate, w_up)

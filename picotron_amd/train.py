@@ -284,9 +284,10 @@ class PipelinedMicroBatchGraph:
 
 
 def pipelined_enabled():
-    """PICO_MB_PIPELINE=1: TrainingStep's graphs replay the step's micro-batches as one two-stream pipelined
-    graph (PipelinedMicroBatchGraph); 0: one MicroBatchGraph replay per micro-batch."""
-    return os.getenv("PICO_MB_PIPELINE", "0") == "1"
+    """TrainingStep's graphs replay the step's micro-batches as one two-stream pipelined graph
+    (PipelinedMicroBatchGraph; default) — PICO_MB_PIPELINE=0: one MicroBatchGraph replay per micro-batch.
+    C2 step, same box, 2 x 2 alternating runs: 865.2 / 866.9 -> 848.8 / 850.0 ms (profiles/r04_ab_pipeline_actt.jsonl)."""
+    return os.getenv("PICO_MB_PIPELINE", "1") != "0"
 
 
 class TrainingStep:

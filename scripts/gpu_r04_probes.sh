@@ -6,8 +6,8 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 timeout -k 10 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_model_gpu.py \
-  tests/test_kernels_gpu.py -k "graph_replay or act_t_only or transposed" > gpurun_out/pipe_tests.log 2>&1 &&
-VARIANTS="base: pipe:PICO_MB_PIPELINE=1 actt:PICO_ACT_T_ONLY=1 both:PICO_MB_PIPELINE=1,PICO_ACT_T_ONLY=1" \
+  tests/test_kernels_gpu.py -k "graph_replay or transposed" > gpurun_out/pipe_tests.log 2>&1 &&
+VARIANTS="base:PICO_MB_PIPELINE=0 pipe:PICO_MB_PIPELINE=1" \
   STEP_ROUNDS=2 STEPS=5 timeout -k 10 1000 bash scripts/gpu_ab_env.sh &&
 timeout -k 10 240 python -u scripts/gemm_at_probe.py > gpurun_out/gemm_at_probe.jsonl 2> gpurun_out/gemm_at_probe.log &&
 timeout -k 10 240 python -u scripts/kernel_bench.py > gpurun_out/kernel_bench_hot.jsonl 2> gpurun_out/kernel_bench_hot.log &&

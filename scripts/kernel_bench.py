@@ -6,9 +6,10 @@ algorithmic GB/s (every input read once + every output written once).
 
   python scripts/kernel_bench.py [--cold] [--iters 50]
 
---cold writes a 1 GiB buffer between launches (untimed: the kernel timer brackets the kernel alone), so
-every launch reads its inputs from HBM instead of the 256 MB MALL / L2 that a back-to-back loop leaves them
-in — the condition the kernels meet inside the training step, where the GEMMs between them evict everything."""
+--cold reads a 1 GiB buffer between launches (untimed: the kernel timer brackets the kernel alone), so every
+launch reads its inputs from HBM instead of the 256 MB MALL / L2 that a back-to-back loop leaves them in.
+--cold-write fills the buffer instead: the caches are then also full of dirty lines whose write-back competes
+with the kernel (round-4 first form; slower than the training step itself: too pessimistic)."""
 import argparse
 import json
 import os
@@ -23,6 +24,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--cold", action="store_true")
+    ap.add_argument("--cold-write", action="store_true")
     args = ap.parse_args()
     iters = args.iters
     from picotron_amd import _lib as L
@@ -97,7 +99,8 @@ def main():
         ("transpose_x", lambda: ops.transpose_2d(x.detach(), out=xt), [L.K_TRANSPOSE]),
         ("transpose_wgu", lambda: ops.transpose_2d(wgu, out=wgut), [L.K_TRANSPOSE]),
     ]
-    flush = torch.empty(1 << 29, dtype=torch.bfloat16, device=dev) if args.cold else None
+    flush = torch.ones(1 << 29, dtype=torch.bfloat16, device=dev) if (args.cold or args.cold_write) else None
+    sink = torch.empty((), dtype=torch.float32, device=dev)
     work = {L.K_RMSNORM_FWD: 4 * T * H * 2 + 4 * T, L.K_RMSNORM_BWD: 4 * T * H * 2 + 4 * T,
             L.K_ROPE: 2 * T * 2 * NH * D * 2, L.K_SWIGLU_FWD: 3 * T * I * 2, L.K_SWIGLU_BWD: 5 * T * I * 2,
             L.K_EMBEDDING_BWD: T * H * 2 + 2 * T * H * 2, L.K_CE_FWD: 2 * T * V * 2}
@@ -115,14 +118,16 @@ def main():
         for k in kids:
             L.prof_enable(k, iters + 8)
         for _ in range(iters):
-            if flush is not None:
+            if args.cold_write:
                 flush.fill_(1.0)
+            elif flush is not None:
+                torch.sum(flush, dtype=torch.float32, out=sink)
             fn()
         torch.cuda.synchronize()
         for k in kids:
             ms, n = L.prof_collect(k)
             us = 1e3 * ms / max(n, 1)
-            out = {"cold": bool(args.cold), "kernel": L.KERNEL_NAMES[k] + ("" if k not in (L.K_TRANSPOSE,) and name not in ("rmsnorm_t", "swiglu_t", "rmsnorm_chain", "rope_k") else ":" + name), "avg_us": round(us, 2), "launches": n}
+            out = {"cold": "write" if args.cold_write else bool(args.cold), "kernel": L.KERNEL_NAMES[k] + ("" if k not in (L.K_TRANSPOSE,) and name not in ("rmsnorm_t", "swiglu_t", "rmsnorm_chain", "rope_k") else ":" + name), "avg_us": round(us, 2), "launches": n}
             if k in work:
                 out["GB_s"] = round(work[k] / (us * 1e-6) / 1e9, 1)
                 out["frac_of_8TBs"] = round(out["GB_s"] / 8000, 3)

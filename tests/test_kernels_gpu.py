@@ -885,12 +885,6 @@ def test_swiglu_fwd_transposed_output(T, I):
     assert torch.equal(h, h_ref)
     assert torch.equal(ht[:, :T], h.t())
     assert bool((ht[:, T:] == 2.0).all())
-    # out = NULL: h^T only (PICO_ACT_T_ONLY), the same h^T
-    ht2 = torch.full((I, T + 16), 2.0, dtype=BF, device=DEV)
-    L.check(L.load().pico_swiglu_fwd_t(L.ptr(gu), L.ptr(gu[:, I:]), None, L.ptr(ht2), T, I, 2 * I, I, T + 16,
-                                       L.stream_of(gu)), "swiglu_fwd_t")
-    torch.cuda.synchronize()
-    assert torch.equal(ht2, ht)
 
 
 @pytest.mark.parametrize("rows,cols,res", [(64, 2048, True), (96, 1024, False), (256, 2048, True), (4096, 2048, True)])
@@ -908,24 +902,4 @@ def test_rmsnorm_fwd_transposed_output(rows, cols, res):
     if res:
         assert torch.equal(out[1], out_ref[1])
     assert torch.equal(y._pico_t, y.t())
-
-
-@pytest.mark.parametrize("rows,cols,res", [(64, 2048, True), (96, 1024, False)])
-def test_rmsnorm_fwd_transposed_only(rows, cols, res, monkeypatch):
-    """PICO_ACT_T_ONLY=1: pico_rmsnorm_fwd_t with y = NULL writes the same y^T / residual_out / rstd, and the
-    returned y is the transposed view of y^T (equal to the row-major y of the default form)."""
-    from picotron_amd import ops
-    torch.manual_seed(rows + cols)
-    x = torch.randn(rows, cols, dtype=BF, device=DEV)
-    r = torch.randn(rows, cols, dtype=BF, device=DEV) if res else None
-    w = (1 + 0.1 * torch.randn(cols, device=DEV)).to(BF)
-    out_ref = ops._RMSNormFn.apply(x, r, w, 1e-5, res, True)
-    monkeypatch.setenv("PICO_ACT_T_ONLY", "1")
-    out = ops._RMSNormFn.apply(x, r, w, 1e-5, res, True)
-    y_ref, y = (out_ref[0], out[0]) if res else (out_ref, out)
-    assert not y.is_contiguous() and y.data_ptr() == y._pico_t.data_ptr()
-    assert torch.equal(y, y_ref)
-    assert torch.equal(y._pico_t, y_ref._pico_t)
-    if res:
-        assert torch.equal(out[1], out_ref[1])
 
