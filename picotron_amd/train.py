@@ -204,13 +204,12 @@ class PipelinedMicroBatchGraph:
 
     def _body(self, inp, tgt):
         from . import ops
-        with ops.no_side_streams():
-            self._pipeline(inp, tgt)
-
-    def _pipeline(self, inp, tgt):
         model, n, acc = self.model, self.n, self.loss_acc
         cur = torch.cuda.current_stream()
-        # slot 0 runs on the capture stream itself, slot 1 on one stream forked from it: with BOTH slots on
+        # no dgrad / wgrad side-stream pairs (ops.dgrad_wgrad) inside the pipeline: a fork from slot 1's stream
+        # crashes the capture (ops.no_side_streams), and on slot 0 alone they measured slower (C2 154.2 -> 152.2 K
+        # tokens/s, profiles/r04_ab_pipeline_side0.jsonl): the other micro-batch already fills the chip.
+        # Slot 0 runs on the capture stream itself, slot 1 on one stream forked from it: with BOTH slots on
         # forked streams (dependencies in both directions between two forked streams) hipStreamEndCapture
         # segfaults on this ROCm (scripts/dbg_event_capture.py reproduces it with plain tensor ops)
         streams = (cur, self.streams[1])
@@ -221,7 +220,7 @@ class PipelinedMicroBatchGraph:
         for i in range(k + 1):
             if i >= 1:  # backward of micro-batch i - 1 (on its forward's stream), after backward i - 2
                 st = streams[(i - 1) % 2]
-                with torch.cuda.stream(st):
+                with torch.cuda.stream(st), ops.no_side_streams():
                     if bwd_done is not None:
                         st.wait_event(bwd_done)
                     loss, folded = losses[i - 1]
@@ -233,7 +232,7 @@ class PipelinedMicroBatchGraph:
                 losses[i - 1] = None
             if i < k:  # forward of micro-batch i, after forward i - 1
                 st = streams[i % 2]
-                with torch.cuda.stream(st):
+                with torch.cuda.stream(st), ops.no_side_streams():
                     if fwd_done is not None:
                         st.wait_event(fwd_done)
                     losses[i] = _forward_loss(model, inp[i], tgt[i], n, acc)

@@ -121,7 +121,7 @@ def main():
             if args.cold_write:
                 flush.fill_(1.0)
             elif flush is not None:
-                torch.sum(flush, dtype=torch.float32, out=sink)
+                torch.sum(flush, dim=0, dtype=torch.float32, out=sink)
             fn()
         torch.cuda.synchronize()
         for k in kids:
