@@ -23,6 +23,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import ops
+from . import wgrad_pair as WP
 from . import process_group_manager as pgm
 
 
@@ -142,12 +143,14 @@ class RMSNorm(nn.Module):
         nn.init.ones_(self.weight)
 
     def forward(self, hidden_states, residual=None, dropout_p=0.0, prenorm=False, residual_in_fp32=False,
-                return_dropout_mask=False):
+                return_dropout_mask=False, _pair=None):
         # the norm outputs of this model feed projections (qkv, gate|up, LM head) whose weight-gradient
-        # GEMM reads y^T: the kernel writes it alongside y (ops._wgrad_input picks it up)
+        # GEMM reads y^T: the kernel writes it alongside y (ops._wgrad_input picks it up). _pair: paired
+        # weight-gradient hints (wgrad_pair; DecoderLayer._pair_hints)
         return ops.layer_norm_fn(hidden_states, self.weight, None, residual=residual, eps=self.eps,
                                  dropout_p=dropout_p, prenorm=prenorm, residual_in_fp32=residual_in_fp32,
-                                 is_rms_norm=True, return_dropout_mask=return_dropout_mask, _emit_transposed=True)
+                                 is_rms_norm=True, return_dropout_mask=return_dropout_mask, _emit_transposed=True,
+                                 _pair=_pair)
 
 
 TritonRMSNorm = RMSNorm
@@ -185,7 +188,7 @@ class Attention(nn.Module):
             return None
         return _col_parallel((self.q_proj, self.k_proj, self.v_proj))
 
-    def forward(self, x, cos, sin, attention_mask=None, position_ids=None):
+    def forward(self, x, cos, sin, attention_mask=None, position_ids=None, out_hint=None):
         require_kernel_path()
         B, S, _ = x.size()
         D = self.head_dim
@@ -195,7 +198,7 @@ class Attention(nn.Module):
             # under TP the local shards, with one f region (input-gradient all-reduce) for all three
             x = _tp_input(kind, x)
             out = ops.qkv_rope_attention(x, self.q_proj.weight, self.k_proj.weight, self.v_proj.weight, cos, sin,
-                                         self.num_local_heads, self.num_local_kv_heads, True)
+                                         self.num_local_heads, self.num_local_kv_heads, True, out_hint=out_hint)
             return _proj(self.out_proj, out)
         q = self.q_proj(x).view(B, S, self.num_local_heads, D)
         k = self.k_proj(x).view(B, S, self.num_local_kv_heads, D)
@@ -229,12 +232,13 @@ class MLP(nn.Module):
             bound = math.sqrt(1 / w.size(1))
             torch.nn.init.uniform_(w, -bound, bound)
 
-    def forward(self, x):
+    def forward(self, x, down_hint=None):
         kind = _col_parallel((self.gate_proj, self.up_proj)) if os.getenv("PICO_UNFUSED", "0") != "1" else None
         if kind is not None:
             # one gate|up GEMM + strided SwiGLU (ops._GateUpSwiGLUFn); under TP on the local shards, one f region
             x = _tp_input(kind, x)
-            return _proj(self.down_proj, ops.gate_up_swiglu(x, self.gate_proj.weight, self.up_proj.weight))
+            return _proj(self.down_proj, ops.gate_up_swiglu(x, self.gate_proj.weight, self.up_proj.weight,
+                                                            down_hint=down_hint))
         return self.down_proj(ops.swiglu(self.gate_proj(x), self.up_proj(x)))
 
 
@@ -269,19 +273,40 @@ class DecoderLayer(nn.Module):
         x = x + self.mlp(self.post_attention_layernorm(x))
         return x
 
-    def forward_fused(self, delta, residual):
+    def _pair_hints(self):
+        """Paired weight-gradient hints (wgrad_pair) of this layer's four projections, (weight, N, K) each — the
+        weight keys its pair buffers — or None when the pairing is off or a projection is not a plain bias-free
+        nn.Linear on the fused paths (TP / CP layers, PICO_UNFUSED)."""
+        if not WP.active() or os.getenv("PICO_UNFUSED", "0") == "1" or os.getenv("CONTEXT_PARALLEL", "0") == "1":
+            return None
+        a, m = self.attention, self.mlp
+        lins = (a.q_proj, a.k_proj, a.v_proj, a.out_proj, m.gate_proj, m.up_proj, m.down_proj)
+        if any(type(t) is not nn.Linear or t.bias is not None for t in lins) or pgm.tp_world_size() > 1:
+            return None
+        hd, inter = a.out_proj.weight.shape[0], m.down_proj.weight.shape[1]
+        nqkv = a.q_proj.weight.shape[0] + a.k_proj.weight.shape[0] + a.v_proj.weight.shape[0]
+        return {"qkv": (a.q_proj.weight, nqkv, a.q_proj.weight.shape[1]),
+                "out": (a.out_proj.weight, hd, a.out_proj.weight.shape[1]),
+                "gu": (m.gate_proj.weight, 2 * m.gate_proj.weight.shape[0], m.gate_proj.weight.shape[1]),
+                "down": (m.down_proj.weight, hd, inter)}
+
+    def forward_fused(self, delta, residual, prev_down=None):
         """Same layer with the residual adds fused into the norms (layer_norm_fn prenorm form):
         the layer input is residual + delta (residual None for the first layer). Returns the
         (delta, residual) pair whose sum is this layer's output; every sum is rounded to bf16 exactly
-        like the reference's `x + f(x)`."""
+        like the reference's `x + f(x)`. prev_down: the previous layer's down-projection pair hint (delta is its
+        output, so the input norm's dx is that projection's dy)."""
+        hints = self._pair_hints()
+        p_in = (hints["qkv"], prev_down) if hints else None
+        p_post = (hints["gu"], hints["out"]) if hints else None
         if residual is None:  # prenorm form without a residual: x is the norm's second output, so the
             # embedding output has one consumer and its gradient needs no separate add
-            h_in, x = self.input_layernorm(delta, residual=None, prenorm=True)
+            h_in, x = self.input_layernorm(delta, residual=None, prenorm=True, _pair=p_in)
         else:
-            h_in, x = self.input_layernorm(delta, residual=residual, prenorm=True)
-        attn = self.attention(h_in, self.cos, self.sin)
-        h2, x = self.post_attention_layernorm(attn, residual=x, prenorm=True)
-        return self.mlp(h2), x
+            h_in, x = self.input_layernorm(delta, residual=residual, prenorm=True, _pair=p_in)
+        attn = self.attention(h_in, self.cos, self.sin, out_hint=hints["out"] if hints else None)
+        h2, x = self.post_attention_layernorm(attn, residual=x, prenorm=True, _pair=p_post)
+        return self.mlp(h2, down_hint=hints["down"] if hints else None), x
 
 
 class Embedding(nn.Module):
@@ -347,9 +372,14 @@ class Llama(nn.Module):
                 x = layer(x)
             return self.final_proj(self.final_norm(x))
         delta, residual = x, None
+        down = None  # the previous layer's down-projection pair hint (wgrad_pair)
         for layer in self.decoder_layers:
-            delta, residual = layer.forward_fused(delta, residual)
-        h = self.final_norm(delta) if residual is None else self.final_norm(delta, residual=residual)
+            delta, residual = layer.forward_fused(delta, residual, prev_down=down)
+            hints = layer._pair_hints()
+            down = hints["down"] if hints else None
+        pair = (None, down) if down is not None else None
+        h = self.final_norm(delta, _pair=pair) if residual is None else \
+            self.final_norm(delta, residual=residual, _pair=pair)
         if return_hidden:
             return h
         return _proj(self.final_proj, h)

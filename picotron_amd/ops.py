@@ -42,7 +42,10 @@ def _need(t, name, dtype=_BF16):
 # --------------------------------------------------------------------------------------------
 class _RMSNormFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, residual, weight, eps, prenorm, want_t=False):
+    def forward(ctx, x, residual, weight, eps, prenorm, want_t=False, pair=None):
+        """pair: (xt_for, dy_for) paired-wgrad hints (wgrad_pair): the (weight, N, K) of the projection that reads
+        y (its x^T goes into that projection's pair buffer) and of the projection whose output is x (dx goes into
+        its dy pair buffer), or None."""
         _need(x, "x")
         _need(weight, "weight")
         # a chained dw left pending while no backward pass runs means the pass that created it raised before its
@@ -67,10 +70,13 @@ class _RMSNormFn(torch.autograd.Function):
         yt = None
         if want_t and os.getenv("PICO_XT_WGRAD", "1") != "0" and cols in (1024, 2048) and rows % 32 == 0 and \
                 all(t is None or t.data_ptr() % 16 == 0 for t in (x2, res2, w)):
-            # y^T as a by-product for the next projection's TT wgrad GEMM (no separate transpose pass)
-            yt = torch.empty((cols, rows), dtype=x.dtype, device=x.device)
+            # y^T as a by-product for the next projection's TT wgrad GEMM (no separate transpose pass), into the
+            # projection's x^T pair buffer when its weight gradients are paired
+            yt = _pair_xt(pair[0] if pair else None, cols, rows, x) if pair else None
+            if yt is None:
+                yt = torch.empty((cols, rows), dtype=x.dtype, device=x.device)
             _lib.check(lib.pico_rmsnorm_fwd_t(_lib.ptr(x2), _lib.ptr(res2), _lib.ptr(w), _lib.ptr(y), _lib.ptr(res_out),
-                                              _lib.ptr(rstd), _lib.ptr(yt), rows, rows, cols, float(eps),
+                                              _lib.ptr(rstd), _lib.ptr(yt), yt.stride(0), rows, cols, float(eps),
                                               _lib.stream_of(x)), "pico_rmsnorm_fwd_t")
         else:
             _lib.check(lib.pico_rmsnorm_fwd(_lib.ptr(x2), _lib.ptr(res2), _lib.ptr(w), _lib.ptr(y), _lib.ptr(res_out),
@@ -82,6 +88,7 @@ class _RMSNormFn(torch.autograd.Function):
         ctx.shape = shape
         ctx.has_residual = residual is not None
         ctx.prenorm = prenorm
+        ctx.pair_dy = pair[1] if pair else None
         y = y.view(shape)
         if yt is not None:
             y._pico_t = yt
@@ -99,7 +106,9 @@ class _RMSNormFn(torch.autograd.Function):
         if ctx.prenorm and rest and rest[0] is not None:
             dres = rest[0].reshape(-1, cols).contiguous()
         lib = _lib.load()
-        dx = torch.empty_like(x_eff)
+        dx = _pair_dy(ctx.pair_dy, rows, cols, x_eff)  # the producing projection's dy pair buffer (wgrad_pair)
+        if dx is None:
+            dx = torch.empty_like(x_eff)
         mode, target, scale, ready = _norm_grad_target(ctx.weight_param, w)
         dw = target if mode == 0 else None
         ws = torch.empty(lib.pico_rmsnorm_bwd_workspace_bytes(rows, cols), dtype=torch.uint8, device=dy.device)
@@ -124,7 +133,7 @@ class _RMSNormFn(torch.autograd.Function):
         elif ready is not None:
             ready()
         dx = dx.view(ctx.shape)
-        return dx, (dx if ctx.has_residual else None), dw, None, None, None
+        return dx, (dx if ctx.has_residual else None), dw, None, None, None, None
 
 
 # device -> a norm backward's dw partial rows waiting for the next norm backward of the same pass to reduce them
@@ -172,13 +181,36 @@ def _norm_grad_target(p, w):
     return 0, torch.empty_like(w), 1.0, None
 
 
+def _pair_xt(hint, K, T, like):
+    """The [K, T] x^T pair-buffer slot (row stride 2T) of the projection `hint` = (weight, N, K') for the current
+    micro-batch, or None (pairing off, or a shape that does not match)."""
+    if hint is None:
+        return None
+    from . import wgrad_pair as WP
+    w, N, Kh = hint
+    if Kh != K or T % 8 != 0:
+        return None
+    return WP.xt_out(w, N, K, T, like.dtype, like.device)
+
+
+def _pair_dy(hint, T, N, like):
+    """The [T, N] dy pair-buffer slot of the projection `hint` = (weight, N', K) for the current micro-batch, or None."""
+    if hint is None:
+        return None
+    from . import wgrad_pair as WP
+    w, Nh, K = hint
+    if Nh != N:
+        return None
+    return WP.dy_out(w, N, K, T, like.dtype, like.device)
+
+
 def rms_norm(x, weight, eps=1e-5, residual=None, prenorm=False):
     return _RMSNormFn.apply(x, residual, weight, eps, prenorm)
 
 
 def layer_norm_fn(x, weight, bias, residual=None, x1=None, weight1=None, bias1=None, eps=1e-6, dropout_p=0.0,
                   rowscale=None, prenorm=False, residual_in_fp32=False, is_rms_norm=False,
-                  return_dropout_mask=False, _emit_transposed=False):
+                  return_dropout_mask=False, _emit_transposed=False, _pair=None):
     """flash-attn 2.5 `layer_norm_fn` restricted to what picotron calls: RMS norm, no bias/dropout
     (ref picotron/model.py:53-64). Returns y, or (y, residual_out) when prenorm=True."""
     if not is_rms_norm:
@@ -189,7 +221,7 @@ def layer_norm_fn(x, weight, bias, residual=None, x1=None, weight1=None, bias1=N
         raise NotImplementedError("picotron_amd.layer_norm_fn: dropout unsupported")
     if residual_in_fp32:
         raise NotImplementedError("picotron_amd.layer_norm_fn: residual_in_fp32 unsupported")
-    return _RMSNormFn.apply(x, residual, weight, eps, prenorm, bool(_emit_transposed))
+    return _RMSNormFn.apply(x, residual, weight, eps, prenorm, bool(_emit_transposed), _pair)
 
 
 # --------------------------------------------------------------------------------------------
@@ -531,6 +563,21 @@ def _side_stream(dev):
     return side
 
 
+def _wgrad_paired(params, dy2, x2):
+    """wgrad_accumulate with paired weight gradients (wgrad_pair): the first micro-batch of a pair whose operands
+    sit in the pair buffers defers its GEMM (a DP readiness callback still marks the parameter as produced by a
+    fused path, so the bucket hook does not add a stale .grad); the second runs one GEMM over both."""
+    from . import wgrad_pair as WP
+    plan = WP.plan(params[0], dy2, x2)
+    if plan[0] == "skip":
+        for p in params:
+            ready = getattr(p, "_pico_wgrad_ready", None)
+            if ready is not None and getattr(p, "main_grad", None) is not None:
+                ready()
+        return (None,) * len(params)
+    return wgrad_accumulate(params, plan[1], plan[2])
+
+
 def dgrad_wgrad(tag, dy2, W, params, x2):
     """(dx, wgrad_accumulate(...)) for one projection; concurrently on two streams when `tag` is enabled
     (joined before returning: everything after the projection's backward sees both results). Joining later
@@ -541,11 +588,11 @@ def dgrad_wgrad(tag, dy2, W, params, x2):
         side = _side_stream(dev)
         side.wait_stream(cur)
         with torch.cuda.stream(side):
-            dws = wgrad_accumulate(params, dy2, x2)
+            dws = _wgrad_paired(params, dy2, x2)
         dx = dgrad(dy2, W, params)
         cur.wait_stream(side)
         return dx, dws
-    return dgrad(dy2, W, params), wgrad_accumulate(params, dy2, x2)
+    return dgrad(dy2, W, params), _wgrad_paired(params, dy2, x2)
 
 
 def sort_ids(flat, vocab):
@@ -916,7 +963,7 @@ class _LinearFn(torch.autograd.Function):
             dx, (dw,) = dgrad_wgrad("o" if w.shape[0] == w.shape[1] else "lin", dy2, w, (w,), x2)
             return dx.view(ctx.xshape), dw
         dx = dgrad(dy2, w, (w,)).view(ctx.xshape) if ctx.needs_input_grad[0] else None
-        dw = wgrad_accumulate((w,), dy2, x2)[0] if ctx.needs_input_grad[1] else None
+        dw = _wgrad_paired((w,), dy2, x2)[0] if ctx.needs_input_grad[1] else None
         return dx, dw
 
 
@@ -960,7 +1007,8 @@ class _GateUpSwiGLUFn(torch.autograd.Function):
     so x's gradient is one GEMM (no sum of two dgrads) and the weight gradient one GEMM."""
 
     @staticmethod
-    def forward(ctx, x, w_gate, w_up):
+    def forward(ctx, x, w_gate, w_up, down_hint=None):
+        """down_hint: (weight, N, K) of the down projection reading h (wgrad_pair: h^T into its x^T pair buffer)."""
         _need(x, "x")
         I = w_gate.shape[0]
         W = stacked_weight((w_gate, w_up))
@@ -972,9 +1020,11 @@ class _GateUpSwiGLUFn(torch.autograd.Function):
         if os.getenv("PICO_XT_WGRAD", "1") != "0" and os.getenv("PICO_SWIGLU_T", "1") != "0" and T % 64 == 0 \
                 and I % 64 == 0 and gu.data_ptr() % 16 == 0:
             # h^T as a by-product (the down projection's wgrad reads it in the TT GEMM form)
-            ht = torch.empty((I, T), dtype=x.dtype, device=x.device)
+            ht = _pair_xt(down_hint, I, T, x)
+            if ht is None:
+                ht = torch.empty((I, T), dtype=x.dtype, device=x.device)
             _lib.check(_lib.load().pico_swiglu_fwd_t(_lib.ptr(gu), _lib.ptr(gu[:, I:]), _lib.ptr(h), _lib.ptr(ht), T, I,
-                                                     2 * I, I, T, _lib.stream_of(gu)), "pico_swiglu_fwd_t")
+                                                     2 * I, I, ht.stride(0), _lib.stream_of(gu)), "pico_swiglu_fwd_t")
         else:
             _swiglu_fwd(gu, gu[:, I:], h, T, I, 2 * I, I)
         ctx.save_for_backward(_wgrad_input(x2, 2 * I, x), gu, W)
@@ -992,14 +1042,16 @@ class _GateUpSwiGLUFn(torch.autograd.Function):
         d = dh.reshape(-1, I)
         if not d.is_contiguous():
             d = d.contiguous()
-        dgu = torch.empty_like(gu)
+        dgu = _pair_dy((ctx.params[0], 2 * I, x2.shape[1]), gu.shape[0], 2 * I, gu)  # gate|up dy pair buffer
+        if dgu is None:
+            dgu = torch.empty_like(gu)
         _swiglu_bwd(d, gu, gu[:, I:], dgu, dgu[:, I:], gu.shape[0], I, 2 * I, I)
         dx, (dwg, dwu) = dgrad_wgrad("gu", dgu, W, ctx.params, x2)
-        return dx.view(ctx.xshape), dwg, dwu
+        return dx.view(ctx.xshape), dwg, dwu, None
 
 
-def gate_up_swiglu(x, w_gate, w_up):
-    return _GateUpSwiGLUFn.apply(x, w_gate, w_up)
+def gate_up_swiglu(x, w_gate, w_up, down_hint=None):
+    return _GateUpSwiGLUFn.apply(x, w_gate, w_up, down_hint)
 
 
 # --------------------------------------------------------------------------------------------
@@ -1135,7 +1187,8 @@ class _QKVRopeAttentionFn(torch.autograd.Function):
     dW = dqkv^T x (one GEMM, rows = dWq | dWk | dWv)."""
 
     @staticmethod
-    def forward(ctx, x, wq, wk, wv, cos, sin, nh, nkv, causal):
+    def forward(ctx, x, wq, wk, wv, cos, sin, nh, nkv, causal, out_hint=None):
+        """out_hint: (weight, N, K) of the out-projection reading O (wgrad_pair: O^T into its x^T pair buffer)."""
         _need(x, "x")
         B, S, Hd = x.shape
         D = wq.shape[0] // nh
@@ -1152,8 +1205,11 @@ class _QKVRopeAttentionFn(torch.autograd.Function):
         _rope_launch(qk, qk, cos, sin, False)
         scale = 1.0 / math.sqrt(D)
         # O^T for the out-projection's wgrad (TT form), written by the attention epilogue for free
-        o_t = torch.empty((nh * D, B * S), dtype=x.dtype, device=x.device) \
-            if os.getenv("PICO_XT_WGRAD", "1") != "0" else None
+        o_t = None
+        if os.getenv("PICO_XT_WGRAD", "1") != "0":
+            o_t = _pair_xt(out_hint, nh * D, B * S, x)
+            if o_t is None:
+                o_t = torch.empty((nh * D, B * S), dtype=x.dtype, device=x.device)
         o, lse = attention_block_fwd(q, k, v, scale, causal, o_t=o_t, rope_q=(cos, sin) if fuse_q else None)
         ctx.save_for_backward(_wgrad_input(x2, N, x), W, qkv, o, lse, cos, sin)
         ctx.params = (wq, wk, wv)
@@ -1170,7 +1226,9 @@ class _QKVRopeAttentionFn(torch.autograd.Function):
         N = W.shape[0]
         heads = qkv.view(B, S, N // D, D)
         q, k, v = heads[:, :, :nh], heads[:, :, nh:nh + nkv], heads[:, :, nh + nkv:]
-        dqkv = torch.empty_like(qkv)
+        dqkv = _pair_dy((ctx.params[0], N, Hd), B * S, N, qkv)  # the q|k|v dy pair buffer (wgrad_pair)
+        if dqkv is None:
+            dqkv = torch.empty_like(qkv)
         dheads = dqkv.view(B, S, N // D, D)
         # RoPE^-1 on dq | dk fused into the attention backward's dQ sum and dK epilogue
         # (PICO_FUSE_ROPE_BWD=0: separate in-place rope launch, for A/B)
@@ -1182,14 +1240,14 @@ class _QKVRopeAttentionFn(torch.autograd.Function):
             dqk = dheads[:, :, : nh + nkv]
             _rope_launch(dqk, dqk, cos, sin, True)
         dx, (dwq, dwk, dwv) = dgrad_wgrad("qkv", dqkv, W, ctx.params, x2)
-        return dx.view(B, S, Hd), dwq, dwk, dwv, None, None, None, None, None
+        return dx.view(B, S, Hd), dwq, dwk, dwv, None, None, None, None, None, None
 
 
-def qkv_rope_attention(x, wq, wk, wv, cos, sin, num_heads, num_kv_heads, causal):
+def qkv_rope_attention(x, wq, wk, wv, cos, sin, num_heads, num_kv_heads, causal, out_hint=None):
     """Fused attention block (projections + RoPE + flash attention); see _QKVRopeAttentionFn."""
     D = wq.shape[0] // num_heads
     return _QKVRopeAttentionFn.apply(x, wq, wk, wv, cos[:, : D // 2], sin[:, : D // 2], num_heads, num_kv_heads,
-                                     causal)
+                                     causal, out_hint)
 
 
 def _check_rope_tables(cos, sin, D):

@@ -1,6 +1,7 @@
 """Training step and loop — semantics of the reference train.py (train_step :29-55, loop :219-259),
 on the gfx950 hot path. Data is synthetic (no network); the model is built by
 picotron_amd.model.build_llama with the reference's init (seed first)."""
+import contextlib
 import os
 import time
 
@@ -8,6 +9,7 @@ import torch
 import torch.nn.functional as F
 
 from . import process_group_manager as pgm
+from . import wgrad_pair as WP
 
 # MI355X bf16 dense MFMA peak: 256 CUs x 4096 FLOP/clk x 2.4 GHz (MI355X_MICROARCH.md; the H100
 # constant of ref picotron/utils.py:42 is 989.5e12)
@@ -83,6 +85,11 @@ def train_step(model, data_loader, device, graphs=None, sync_loss=True):
     losses = []
     n = data_loader.grad_acc_steps
     grouped = graphs is not None and getattr(graphs, "grouped", False)
+    # paired weight gradients (wgrad_pair) need every micro-batch announced with its index: eager micro-batches and
+    # the pipelined graph do; MicroBatchGraph replays one captured micro-batch for every index, so not with it
+    pair = graphs is None or grouped
+    if pair:
+        WP.begin_step()
     pending = []  # grouped graphs: the non-syncing micro-batches, replayed together before the syncing one
 
     def run_pending():
@@ -106,7 +113,8 @@ def train_step(model, data_loader, device, graphs=None, sync_loss=True):
         if graphs is not None and not sync:  # syncing micro-batches launch RCCL from hooks: eager
             graphs.replay(input_ids, target_ids)
         else:
-            losses.append(_micro_batch(model, input_ids, target_ids, n))
+            with (WP.micro_batch(i, n) if pair else contextlib.nullcontext()):
+                losses.append(_micro_batch(model, input_ids, target_ids, n))
     run_pending()
     if graphs is not None:
         losses.append(graphs.take_loss())
@@ -220,7 +228,7 @@ class PipelinedMicroBatchGraph:
         for i in range(k + 1):
             if i >= 1:  # backward of micro-batch i - 1 (on its forward's stream), after backward i - 2
                 st = streams[(i - 1) % 2]
-                with torch.cuda.stream(st), ops.no_side_streams():
+                with torch.cuda.stream(st), ops.no_side_streams(), WP.micro_batch(i - 1, n):
                     if bwd_done is not None:
                         st.wait_event(bwd_done)
                     loss, folded = losses[i - 1]
@@ -232,7 +240,7 @@ class PipelinedMicroBatchGraph:
                 losses[i - 1] = None
             if i < k:  # forward of micro-batch i, after forward i - 1
                 st = streams[i % 2]
-                with torch.cuda.stream(st), ops.no_side_streams():
+                with torch.cuda.stream(st), ops.no_side_streams(), WP.micro_batch(i, n):
                     if fwd_done is not None:
                         st.wait_event(fwd_done)
                     losses[i] = _forward_loss(model, inp[i], tgt[i], n, acc)
@@ -261,18 +269,21 @@ class PipelinedMicroBatchGraph:
         torch.cuda.synchronize()
         self.zero_grads()
         self.loss_acc.zero_()
-        self.graphs[len(batches)] = (g, inp, tgt)
+        # a first half the graph's last micro-batch leaves deferred (wgrad_pair) for the eager one after it: the
+        # replay runs no Python, so run() re-announces it after every replay
+        self.graphs[len(batches)] = (g, inp, tgt, WP.pending_state())
 
     def run(self, batches):
         from . import ops
         ops.refresh_weight_transposes()  # dgrad W^T copies are graph inputs: bring them up to date
         if len(batches) not in self.graphs:
             self._capture(batches)
-        g, inp, tgt = self.graphs[len(batches)]
+        g, inp, tgt, pending = self.graphs[len(batches)]
         for j, (x, y) in enumerate(batches):
             inp[j].copy_(x)
             tgt[j].copy_(y)
         g.replay()
+        WP.restore_pending(pending)
 
     def take_loss(self):
         if self.loss_acc is None:

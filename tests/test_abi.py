@@ -235,3 +235,59 @@ def test_train_step_groups_non_syncing_micro_batches():
     loader = SyntheticDataLoader(2, 16, 4, 64, seed=3, num_batches=4)
     train_step(m, loader, "cpu", graphs=Grouped(m))
     assert m.log == [("group", False, firsts[:3]), ("eager", True, firsts[3])], m.log
+
+
+def test_wgrad_pair_plan():
+    """wgrad_pair's decisions (host logic, CPU tensors): the first micro-batch of a pair whose operands sit in the
+    pair buffers defers, the second runs one GEMM over both halves; no partner (odd grad_acc) or operands elsewhere
+    -> its own GEMM; a second half not in place while its first half is pending is copied in; pairing off outside
+    an announced micro-batch; a shape change with a first half pending raises."""
+    from picotron_amd import wgrad_pair as WP
+    w = torch.nn.Parameter(torch.zeros(6, 4))
+    N, K, T = 6, 4, 8
+
+    def operands(i):
+        dy = WP.dy_out(w, N, K, T, torch.float32, torch.device("cpu"))
+        xt = WP.xt_out(w, N, K, T, torch.float32, torch.device("cpu"))
+        dy.copy_(torch.full_like(dy, float(i + 1)))
+        xt.copy_(torch.full_like(xt, float(10 * (i + 1))))
+        return dy, xt.t()
+
+    WP.begin_step()
+    with WP.micro_batch(0, 3):
+        dy, x = operands(0)
+        assert WP.plan(w, dy, x) == ("skip",)
+    with WP.micro_batch(1, 3):
+        dy, x = operands(1)
+        kind, dyp, xp = WP.plan(w, dy, x)
+        assert kind == "gemm" and dyp.shape == (2 * T, N) and xp.shape == (2 * T, K)
+        assert torch.equal(dyp[:T], torch.full((T, N), 1.0)) and torch.equal(dyp[T:], torch.full((T, N), 2.0))
+        assert torch.equal(xp[:T], torch.full((T, K), 10.0)) and torch.equal(xp[T:], torch.full((T, K), 20.0))
+    with WP.micro_batch(2, 3):  # no partner: its own GEMM
+        dy, x = operands(2)
+        kind, dyp, xp = WP.plan(w, dy, x)
+        assert kind == "gemm" and dyp.data_ptr() == dy.data_ptr() and xp.shape == (T, K)
+    # a second half whose operands are elsewhere: copied into the pair buffers, one GEMM over both
+    WP.begin_step()
+    with WP.micro_batch(0, 2):
+        dy, x = operands(0)
+        assert WP.plan(w, dy, x) == ("skip",)
+    with WP.micro_batch(1, 2):
+        dy2, x2 = torch.full((T, N), 7.0), torch.full((T, K), 70.0)
+        kind, dyp, xp = WP.plan(w, dy2, x2)
+        assert kind == "gemm" and torch.equal(dyp[T:], dy2) and torch.equal(xp[T:], x2)
+        assert torch.equal(dyp[:T], torch.full((T, N), 1.0))
+    # outside an announced micro-batch: no pairing
+    assert not WP.active() and WP.xt_out(w, N, K, T, torch.float32, torch.device("cpu")) is None
+    dy3, x3 = torch.ones(T, N), torch.ones(T, K)
+    assert WP.plan(w, dy3, x3)[1] is dy3
+    # a pending first half, then buffers of another shape for the same weight: refused loudly
+    WP.begin_step()
+    with WP.micro_batch(0, 2):
+        dy, x = operands(0)
+        assert WP.plan(w, dy, x) == ("skip",)
+    with WP.micro_batch(1, 2):
+        import pytest
+        with pytest.raises(RuntimeError, match="one shape"):
+            WP.dy_out(w, N, K, 2 * T, torch.float32, torch.device("cpu"))
+    WP.begin_step()

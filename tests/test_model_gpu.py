@@ -240,6 +240,78 @@ def test_micro_batch_fused_lm_head_ce(golden_loss, monkeypatch, chunk):
         assert rel_l2(outs["1"][1][n].cpu(), outs["0"][1][n].cpu()) < 3e-2, n
 
 
+_PAIR_CFG = dict(hidden_size=1024, intermediate_size=2048, num_attention_heads=16, num_key_value_heads=16,
+                 num_hidden_layers=2, vocab_size=512, max_position_embeddings=128)
+
+
+@pytest.mark.parametrize("n,dp,graph", [(4, False, False), (3, False, False), (4, True, False), (4, False, True),
+                                        (3, True, True)])
+def test_wgrad_pairs_match_unpaired(monkeypatch, n, dp, graph):
+    """Paired weight gradients (wgrad_pair: two micro-batches' wgrad GEMMs as one over both, the producers writing
+    x^T / dy straight into the pair buffers) == the unpaired loop (PICO_WGRAD_PAIR=0): the loss bit for bit (the
+    forward is unchanged), every gradient / main_grad within fp32-summation tolerance; eager and pipelined graph,
+    with and without DataParallelBucket (RCCL, W = 1), even and odd grad_acc; hidden 1024 so the RMSNorm's y^T
+    form (a pair producer) runs. Also checks that the pairing happened: per step, every pair of micro-batches
+    defers 4 GEMMs per layer and pairs them."""
+    import torch.distributed as dist
+    from picotron_amd import process_group_manager as pgm
+    from picotron_amd import wgrad_pair as WP
+    from picotron_amd.data import SyntheticDataLoader
+    from picotron_amd.data_parallel.data_parallel import DataParallelBucket
+    from picotron_amd.model import LlamaConfig, build_llama
+    from picotron_amd.train import PipelinedMicroBatchGraph, train_step
+    from conftest import rel_l2
+    cfg = LlamaConfig(**_PAIR_CFG)
+    if dp:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0", WORLD_SIZE="1",
+                          LOCAL_RANK="0")
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+        pgm.setup_process_group_manager(1, 1, 1, 1)
+    try:
+        res = {}
+        for mode in ("0", "1"):
+            monkeypatch.setenv("PICO_WGRAD_PAIR", mode)
+            torch.manual_seed(7)
+            m = build_llama(cfg, "cuda", BF)
+            with torch.no_grad():
+                m.final_proj.weight.normal_(0, 0.02, generator=torch.Generator("cuda").manual_seed(1))
+            model = DataParallelBucket(m, bucket_cap_mb=1) if dp else m
+            loader = SyntheticDataLoader(2, 128, n, cfg.vocab_size, seed=5, num_batches=n, device="cuda")
+            for p in m.parameters():
+                p.grad = torch.zeros_like(p)
+
+            def zero():
+                for p in m.parameters():
+                    if p.grad is not None:
+                        p.grad.zero_()
+                if dp:
+                    model.bucket_manager.reset()
+            g = PipelinedMicroBatchGraph(model, n, zero) if graph else None
+            s0 = dict(WP.STATS)
+            zero()
+            loss = train_step(model, loader, "cuda", graphs=g)
+            if graph:  # a second step: the replay (and the eager syncing micro-batch after it) with pairs again
+                zero()
+                loss = train_step(model, loader, "cuda", graphs=g)
+            torch.cuda.synchronize()
+            d = {k: WP.STATS[k] - s0[k] for k in s0}
+            grads = {nme: (p.main_grad.clone() if dp else p.grad.float().clone()) for nme, p in m.named_parameters()}
+            res[mode] = (loss, grads, d)
+        assert res["0"][0] == res["1"][0], (res["0"][0], res["1"][0])
+        assert res["0"][2] == {"deferred": 0, "paired": 0}
+        pairs = (n // 2) * 4 * cfg.num_hidden_layers
+        if graph:  # decisions are taken while capturing (warm-up + capture), replays run no Python
+            assert res["1"][2]["paired"] >= pairs and res["1"][2]["deferred"] == res["1"][2]["paired"], res["1"][2]
+        else:
+            assert res["1"][2] == {"deferred": pairs, "paired": pairs}, res["1"][2]
+        for nme in res["0"][1]:
+            assert rel_l2(res["1"][1][nme].float().cpu(), res["0"][1][nme].float().cpu()) < 5e-3, nme
+    finally:
+        if dp:
+            pgm.process_group_manager = None
+            dist.destroy_process_group()
+
+
 def _train_grads(cfg, toks, fusion, monkeypatch, dp=None):
     """grad_acc = len(toks) micro-batches; returns {name: fp32 grad (or main_grad with DP)}."""
     from picotron_amd.model import build_llama
@@ -387,7 +459,7 @@ def test_wt_refresh_once_per_weight_per_step(golden_loss):
 
 
 @pytest.mark.parametrize("kind", ["per_micro_batch", "pipelined"])
-def test_graph_replay_matches_eager(golden_loss, kind):
+def test_graph_replay_matches_eager(golden_loss, kind, monkeypatch):
     """MicroBatchGraph (HIP-graph replay of forward + CE + backward) — or PipelinedMicroBatchGraph (the step's
     micro-batches as one graph, forward i beside backward i - 1 on two streams) — gives the eager loop's loss
     and gradients bit for bit over a 3-micro-batch step, and a second step after an optimizer update."""
@@ -395,6 +467,8 @@ def test_graph_replay_matches_eager(golden_loss, kind):
     from picotron_amd.model import build_llama
     from picotron_amd.train import MicroBatchGraph, PipelinedMicroBatchGraph, train_step
     cls = PipelinedMicroBatchGraph if kind == "pipelined" else MicroBatchGraph
+    if kind == "per_micro_batch":  # MicroBatchGraph cannot pair weight gradients: compare with the unpaired loop
+        monkeypatch.setenv("PICO_WGRAD_PAIR", "0")
     cfg = _cfg(golden_loss)
     results = []
     for use_graph in (False, True):
@@ -427,7 +501,7 @@ def test_graph_replay_matches_eager(golden_loss, kind):
 
 
 @pytest.mark.parametrize("kind", ["per_micro_batch", "pipelined"])
-def test_graph_replay_with_dp_bucket(golden_loss, kind):
+def test_graph_replay_with_dp_bucket(golden_loss, kind, monkeypatch):
     """DataParallelBucket (RCCL, W = 1) + MicroBatchGraph (or PipelinedMicroBatchGraph): the non-syncing
     micro-batches replay as a graph (their DP hooks' accumulates are captured), the syncing one runs eagerly;
     main_grad, .grad and the updated parameters equal the all-eager loop bit for bit, over two steps."""
@@ -438,6 +512,8 @@ def test_graph_replay_with_dp_bucket(golden_loss, kind):
     from picotron_amd.model import build_llama
     from picotron_amd.train import MicroBatchGraph, PipelinedMicroBatchGraph, train_step
     cls = PipelinedMicroBatchGraph if kind == "pipelined" else MicroBatchGraph
+    if kind == "per_micro_batch":
+        monkeypatch.setenv("PICO_WGRAD_PAIR", "0")
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0", WORLD_SIZE="1",
                       LOCAL_RANK="0")
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
