@@ -231,6 +231,7 @@ def main():
     elapsed = time.perf_counter() - t_start
     losses = [float(l) for l in losses]
     from picotron_amd import ops as _ops
+    from picotron_amd import wgrad_pair as _WP
     _ops.check_lm_head_grad_scale()  # the chunked CE's unit-upstream contract held over the timed steps
     t = torch.tensor([elapsed], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -342,7 +343,9 @@ def main():
                        "seq_len": SEQ, "micro_batch": MBS, "grad_acc": args.grad_acc, "parallelism": f"dp{world}",
                        "schedule": ("eager" if not args.graphs else
                                     "pipelined graph (forward i beside backward i-1)" if pipelined_enabled() else
-                                    "graph per micro-batch")},
+                                    "graph per micro-batch"),
+                       "wgrad": ("paired micro-batches (one GEMM per projection per two micro-batches)"
+                                 if _WP.enabled() and (not args.graphs or pipelined_enabled()) else "per micro-batch")},
             "tokens_per_sec_per_gpu": round(tps_gpu, 1),
             "mfu_pct": round(mfu, 2),
             "mfu_peak_tflops": round(BF16_PEAK_TFLOPS, 1),
