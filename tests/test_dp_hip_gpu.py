@@ -235,9 +235,13 @@ def _c3_ref_worker(rank, world, port, out_path):
         ld = SyntheticDataLoader(bench.MBS, bench.SEQ, C3_GA, cfg.vocab_size, seed=1234, kind="uniform",
                                  num_batches=C3_GA, device=dev, dp_rank=r)
         batches += [next(ld) for _ in range(C3_GA)]
+    from picotron_amd import wgrad_pair as WP
     for i, b in enumerate(batches):
         model.require_backward_grad_sync = i == len(batches) - 1
-        _micro_batch(model, b["input_ids"], b["target_ids"], C3_GA)
+        # each rank's grad_acc micro-batches announced as its train_step does, so their weight gradients pair the
+        # same way (wgrad_pair: one GEMM, one bf16 rounding of a multi-parameter projection's dW per pair)
+        with WP.micro_batch(i % C3_GA, C3_GA):
+            _micro_batch(model, b["input_ids"], b["target_ids"], C3_GA)
     torch.cuda.synchronize()
     torch.save([g.cpu() for g in model.bucket_manager.grad_data_list], out_path)
     print("[c3 ref] one-process sum over 8 x 2 micro-batches saved", file=sys.stderr, flush=True)
