@@ -21,13 +21,15 @@ SHAPES = {  # name: (N out rows, K in cols, x kept transposed)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=30)
+    ap.add_argument("--tokens", default="4096,8192", help="comma list of T")
     args = ap.parse_args()
+    TOKENS = [int(t) for t in args.tokens.split(",")]
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
     for name, (N, K, xt) in SHAPES.items():
         g = torch.zeros(N, K, device=dev, dtype=torch.bfloat16)
         res = {"gemm": name, "N": N, "K": K}
-        for T in (4096, 8192):
+        for T in TOKENS:
             dy = torch.randn(T, N, device=dev, dtype=torch.bfloat16)
             x = torch.randn(K, T, device=dev, dtype=torch.bfloat16).t() if xt else \
                 torch.randn(T, K, device=dev, dtype=torch.bfloat16)
@@ -44,7 +46,10 @@ def main():
                 best = min(best, 1e3 * e0.elapsed_time(e1) / args.iters)
             res[f"T{T}_us"] = round(best, 2)
             res[f"T{T}_tflops"] = round(2.0 * T * N * K / best / 1e6, 1)
-        res["two_4096_vs_one_8192_us"] = [round(2 * res["T4096_us"], 2), res["T8192_us"]]
+        if "T4096_us" in res and "T8192_us" in res:
+            res["two_4096_vs_one_8192_us"] = [round(2 * res["T4096_us"], 2), res["T8192_us"]]
+        if "T4096_us" in res and "T16384_us" in res:
+            res["four_4096_vs_one_16384_us"] = [round(4 * res["T4096_us"], 2), res["T16384_us"]]
         print(json.dumps(res), flush=True)
 
 
