@@ -1042,7 +1042,8 @@ class _GateUpSwiGLUFn(torch.autograd.Function):
         d = dh.reshape(-1, I)
         if not d.is_contiguous():
             d = d.contiguous()
-        dgu = _pair_dy((ctx.params[0], 2 * I, x2.shape[1]), gu.shape[0], 2 * I, gu)  # gate|up dy pair buffer
+        from . import wgrad_pair as WP
+        dgu = WP.dy_out_if_paired(ctx.params[0], x2, 2 * I, x2.shape[1], gu.shape[0], gu.dtype, gu.device)
         if dgu is None:
             dgu = torch.empty_like(gu)
         _swiglu_bwd(d, gu, gu[:, I:], dgu, dgu[:, I:], gu.shape[0], I, 2 * I, I)
@@ -1226,7 +1227,9 @@ class _QKVRopeAttentionFn(torch.autograd.Function):
         N = W.shape[0]
         heads = qkv.view(B, S, N // D, D)
         q, k, v = heads[:, :, :nh], heads[:, :, nh:nh + nkv], heads[:, :, nh + nkv:]
-        dqkv = _pair_dy((ctx.params[0], N, Hd), B * S, N, qkv)  # the q|k|v dy pair buffer (wgrad_pair)
+        from . import wgrad_pair as WP
+        # the q|k|v dy pair buffer when the forward paired this micro-batch's x^T (wgrad_pair)
+        dqkv = WP.dy_out_if_paired(ctx.params[0], x2, N, Hd, B * S, qkv.dtype, qkv.device)
         if dqkv is None:
             dqkv = torch.empty_like(qkv)
         dheads = dqkv.view(B, S, N // D, D)

@@ -126,6 +126,17 @@ def dy_out(weight, N, K, T, dtype, device):
     return buf(weight, N, K, T, dtype, device).dy_slot(_CTX["i"])
 
 
+def dy_out_if_paired(weight, x2, N, K, T, dtype, device):
+    """dy_out, but only when this micro-batch's x^T of `weight` (x2, the [T, K] view its backward saved) sits in the
+    weight's pair buffer — i.e. the forward paired it; otherwise None (no buffers created for unpaired paths)."""
+    if not active() or weight is None:
+        return None
+    b = _get(weight)
+    if b is None or (b.N, b.K, b.T) != (N, K, T) or x2.data_ptr() != b.xt_slot(_CTX["i"]).data_ptr():
+        return None
+    return b.dy_slot(_CTX["i"])
+
+
 def plan(weight, dy2, x2):
     """How the wgrad of `weight` runs for the current micro-batch: ('skip',) — first half, deferred; or
     ('gemm', dy, x) — one GEMM over (dy, x): the pair, or this micro-batch alone. A second half whose own operands
