@@ -11,11 +11,12 @@ dx) — write straight into per-projection pair buffers, micro-batch i into half
     dy pair   [2T, N]  (one set: the backwards run in micro-batch order)
 
 The first micro-batch of a pair then skips its wgrad GEMM and the second runs dW (+)= dy_pair^T x_pair over
-K = 2T tokens — hipBLASLt runs the doubled-K GEMM 8-17 % faster than two GEMMs (scripts/gemm_wgrad_k_probe.py),
+K = 2T tokens — hipBLASLt runs the doubled-K GEMM 3-17 % faster than two GEMMs (scripts/gemm_wgrad_k_probe.py),
 with no copy: the operands are already adjacent. dW is the same sum, accumulated in one fp32 GEMM instead of two
 (one bf16 rounding of the .grad accumulate per pair instead of per micro-batch). A micro-batch without a partner
-(the last of an odd grad_acc) runs its own GEMM; so does any micro-batch whose operands are not in the pair
-halves (the pairing is verified per GEMM by pointer, never assumed), which also collects a deferred first half.
+(the last of an odd grad_acc) runs its own GEMM, as does a first half whose operands are not in its pair halves
+(the pairing is verified per GEMM by pointer, never assumed); a second half whose own operands are elsewhere while
+its first half is pending copies them in and runs the pair GEMM.
 
 Active only inside train.train_step / PipelinedMicroBatchGraph, which announce each micro-batch
 (`micro_batch(i, n)`), and with PICO_WGRAD_PAIR != 0. Not under MicroBatchGraph: its one captured micro-batch
