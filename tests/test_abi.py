@@ -291,3 +291,50 @@ def test_wgrad_pair_plan():
         with pytest.raises(RuntimeError, match="one shape"):
             WP.dy_out(w, N, K, 2 * T, torch.float32, torch.device("cpu"))
     WP.begin_step()
+
+
+def test_train_step_announces_micro_batches():
+    """train_step announces each eager micro-batch's index to wgrad_pair (the pairing's only source of truth), and
+    none under a per-micro-batch graph object (MicroBatchGraph cannot pair); PICO_WGRAD_PAIR=0 announces nothing."""
+    import os
+    from picotron_amd import wgrad_pair as WP
+    from picotron_amd.data import SyntheticDataLoader
+    from picotron_amd.train import train_step
+
+    class Tiny(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.emb = torch.nn.Embedding(64, 8)
+            self.out = torch.nn.Linear(8, 64, bias=False)
+            self.seen = []
+
+        def forward(self, input_ids):
+            self.seen.append((WP._CTX["i"], WP._CTX["n"]))
+            return self.out(self.emb(input_ids))
+
+    m = Tiny()
+    train_step(m, SyntheticDataLoader(2, 16, 3, 64, seed=3, num_batches=3), "cpu")
+    assert m.seen == [(0, 3), (1, 3), (2, 3)], m.seen
+    assert WP._CTX["i"] is None
+
+    class PerMB:
+        def replay(self, x, y):
+            m(input_ids=x)
+
+        def take_loss(self):
+            return torch.zeros(())
+
+    m.seen.clear()
+    train_step(m, SyntheticDataLoader(2, 16, 2, 64, seed=3, num_batches=2), "cpu", graphs=PerMB())
+    assert m.seen == [(None, None), (None, None)], m.seen
+    old = os.environ.get("PICO_WGRAD_PAIR")
+    os.environ["PICO_WGRAD_PAIR"] = "0"
+    try:
+        m.seen.clear()
+        train_step(m, SyntheticDataLoader(2, 16, 2, 64, seed=3, num_batches=2), "cpu")
+        assert m.seen == [(None, None), (None, None)], m.seen
+    finally:
+        if old is None:
+            del os.environ["PICO_WGRAD_PAIR"]
+        else:
+            os.environ["PICO_WGRAD_PAIR"] = old
