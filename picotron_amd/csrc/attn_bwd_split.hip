@@ -17,7 +17,7 @@
 //     MFMA's C operand), dQ^T += K^T dS^T (A = transposed reads of the same K image, B = the dS^T
 //     accumulator packed to bf16 in place). It also computes delta = rowsum(dO*O) from registers and
 //     writes delta / LSE*log2(e) for the second kernel (no separate pre-pass).
-//   attn_bwd_kv_kernel: one workgroup = 4 waves x 64 keys = 256 keys of one (batch, kv-head),
+//   attn_bwd_kv_kernel: one workgroup = 4 waves x 32 keys = 128 keys of one (batch, kv-head),
 //     sweeping (query head of the group) x 32-row query tiles (Q, dO, LSE/delta by LDS-DMA). Key on
 //     the lane: S = Q K^T, dP = dO V^T (K, V fragments resident in registers), then dV^T += dO^T P and
 //     dK^T += Q^T dS with the P / dS accumulators as B operands (no LDS round trip at all).
