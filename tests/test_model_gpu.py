@@ -581,3 +581,44 @@ def test_bench_dp2_gloo_on_one_gpu():
     assert math.isfinite(out["loss_last"]) and out["loss_last"] < math.log(49152) + 0.1
     ar = out["allreduce"]
     assert ar["buckets"] > 0 and ar["bytes"] > 0 and ar["busbw_GBps"] > 0
+
+
+def test_smollm_step_pipelined_paired_matches_eager(monkeypatch):
+    """bench.py's step at SmolLM-1.7B geometry (2 layers, seq 1024, micro-batch 4, grad_acc 4; hidden 2048 so the
+    RMSNorm y^T kernel and every pair producer run at the bench's shapes): TrainingStep's pipelined graph with paired
+    weight gradients vs the eager, unpaired loop — the loss bit for bit, every gradient within the pairing's bf16
+    rounding (rel-L2 < 5e-3), the optimizer step then applied to both."""
+    import bench
+    from picotron_amd import process_group_manager as pgm
+    from picotron_amd.train import TrainingStep
+    from conftest import rel_l2
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        pgm.setup_process_group_manager(1, 1, 1, 1)
+        dev = torch.device("cuda", 0)
+
+        def head(m):
+            with torch.no_grad():
+                m.final_proj.weight.normal_(0, 0.02, generator=torch.Generator("cuda").manual_seed(1))
+        res = {}
+        for mode in ("eager", "graph"):
+            monkeypatch.setenv("PICO_WGRAD_PAIR", "0" if mode == "eager" else "1")
+            cfg, model, opt, loader, _ = bench.setup(2, 4, 1, dev, post_build=head)
+            step = TrainingStep(model, opt, loader, dev, graphs=mode == "graph")
+            step.zero()
+            loss = step.micro_batches()
+            torch.cuda.synchronize()
+            grads = {n: p.grad.float().clone() for n, p in model.named_parameters()}
+            step.optimizer_step()
+            torch.cuda.synchronize()
+            res[mode] = (loss, grads, {n: p.detach().float().clone() for n, p in model.named_parameters()})
+            del step, model, opt
+        assert res["eager"][0] == res["graph"][0], (res["eager"][0], res["graph"][0])
+        for n in res["eager"][1]:
+            assert rel_l2(res["graph"][1][n].cpu(), res["eager"][1][n].cpu()) < 5e-3, n
+            assert rel_l2(res["graph"][2][n].cpu(), res["eager"][2][n].cpu()) < 1e-2, n
+    finally:
+        pgm.process_group_manager = None
+        dist.destroy_process_group()
