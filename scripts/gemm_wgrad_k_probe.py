@@ -22,13 +22,16 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=30)
     ap.add_argument("--tokens", default="4096,8192", help="comma list of T")
+    ap.add_argument("--layouts", default="t", help="x operand layouts: t (the transposed view of a stored x^T, the "
+                                                     "step's form), r (row-major x), or t,r")
     args = ap.parse_args()
     TOKENS = [int(t) for t in args.tokens.split(",")]
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
-    for name, (N, K, xt) in SHAPES.items():
+    for (name, (N, K, _)), lay in [(it, lay) for it in SHAPES.items() for lay in args.layouts.split(",")]:
+        xt = lay == "t"
         g = torch.zeros(N, K, device=dev, dtype=torch.bfloat16)
-        res = {"gemm": name, "N": N, "K": K}
+        res = {"gemm": name, "N": N, "K": K, "x_layout": "x^T stored" if xt else "x row-major"}
         for T in TOKENS:
             dy = torch.randn(T, N, device=dev, dtype=torch.bfloat16)
             x = torch.randn(K, T, device=dev, dtype=torch.bfloat16).t() if xt else \
