@@ -101,15 +101,17 @@ class _CycledLoader:
         return {"input_ids": t[:, :-1], "target_ids": t[:, 1:]}
 
 
-def test_loss_curve_shipped_path_overlays_reference(golden_loss):
+@pytest.mark.parametrize("kind", ["pipelined", "per_micro_batch"])
+def test_loss_curve_shipped_path_overlays_reference(golden_loss, kind):
     """The 200-step overlay through exactly what bench.py times: train.train_step with
-    the fused LM-head + cross-entropy (_micro_batch), every micro-batch replayed from one HIP graph
-    (MicroBatchGraph), picotron_amd.optim.AdamW (pico_adamw_bf16), zero_grad(set_to_none=False) — against
-    the reference's bf16 curve, with the bounds of test_loss_curve_overlays_reference."""
+    the fused LM-head + cross-entropy (_micro_batch), the micro-batches replayed from HIP graphs — the shipped
+    PipelinedMicroBatchGraph (two-stream pipeline, paired weight gradients) and MicroBatchGraph —,
+    picotron_amd.optim.AdamW (pico_adamw_bf16), zero_grad(set_to_none=False) — against the reference's bf16 curve,
+    with the bounds of test_loss_curve_overlays_reference."""
     from picotron_amd.data import synth_tokens
     from picotron_amd.model import build_llama
     from picotron_amd.optim import AdamW
-    from picotron_amd.train import MicroBatchGraph, train_step
+    from picotron_amd.train import MicroBatchGraph, PipelinedMicroBatchGraph, train_step
     cfg = golden_loss["config"]
     torch.manual_seed(golden_loss["seed"])
     m = build_llama(_cfg(golden_loss), device="cuda", dtype=BF)
@@ -122,7 +124,7 @@ def test_loss_curve_shipped_path_overlays_reference(golden_loss):
         for p in m.parameters():
             if p.grad is not None:
                 p.grad.zero_()
-    graphs = MicroBatchGraph(m, ga, zero)
+    graphs = (PipelinedMicroBatchGraph if kind == "pipelined" else MicroBatchGraph)(m, ga, zero)
     losses = []
     for _ in range(200):
         opt.zero_grad(set_to_none=False)
@@ -132,7 +134,7 @@ def test_loss_curve_shipped_path_overlays_reference(golden_loss):
     out = os.environ.get("PICO_LOSS_OUT")
     if out:
         import json
-        with open(out.replace(".json", "_shipped.json"), "w") as f:
+        with open(out.replace(".json", f"_shipped_{kind}.json"), "w") as f:
             json.dump({"gpu_bf16_shipped_path": losses, "reference_cpu_bf16": ref}, f)
     # step 0 = ln V up to the bf16 rounding of each micro-batch's loss (the fused CE returns the loss in the
     # logits' dtype, as ATen's does: ln 512 / 2 lies in [2, 4), 1 bf16 ulp = 0.0156)
