@@ -613,12 +613,13 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kv_kernel(const pico_
     }
   };
   // V: P = exp2(S scale log2e - LSE log2e), dS = P dP, packed to bf16 (the B operands of M2)
-  auto vsm = [&](int si, const f32x16 (&s)[KH], const f32x16 (&dp)[KH], bf16x8 (&pf)[KH][2], bf16x8 (&sf)[KH][2])
-      __attribute__((always_inline)) {
+  auto read_l2 = [&](int si, f32x4 (&l2)[4]) __attribute__((always_inline)) {
     const float* lsd = (const float*)(smem + (unsigned)si * (unsigned)C::SLOT + 2 * C::QIMG);
-    f32x4 l2[4];
 #pragma unroll
     for (int g = 0; g < 4; ++g) l2[g] = *reinterpret_cast<const f32x4*>(lsd + 8 * g + 4 * h);
+  };
+  auto vsm_l2 = [&](const f32x4 (&l2)[4], const f32x16 (&s)[KH], const f32x16 (&dp)[KH], bf16x8 (&pf)[KH][2],
+                    bf16x8 (&sf)[KH][2]) __attribute__((always_inline)) {
 #pragma unroll
     for (int kt = 0; kt < KH; ++kt) {
       float pv[16], sv[16];
@@ -632,6 +633,12 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kv_kernel(const pico_
       sf[kt][0] = pack_bf16x8(sv);
       sf[kt][1] = pack_bf16x8(sv + 8);
     }
+  };
+  auto vsm = [&](int si, const f32x16 (&s)[KH], const f32x16 (&dp)[KH], bf16x8 (&pf)[KH][2], bf16x8 (&sf)[KH][2])
+      __attribute__((always_inline)) {
+    f32x4 l2[4];
+    read_l2(si, l2);
+    vsm_l2(l2, s, dp, pf, sf);
   };
   // M2: dV^T[d][key] += dO^T[d][q] P[q][key], dK^T[d][key] += Q^T[d][q] dS[q][key] (A = transposed reads)
   auto m2 = [&](int si, const bf16x8 (&pf)[KH][2], const bf16x8 (&sf)[KH][2]) __attribute__((always_inline)) {
@@ -676,8 +683,37 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kv_kernel(const pico_
       f32x16 s[KH], dp[KH];
       bf16x8 pf[KH][2], sf[KH][2];
       m1(u, q0cur, s, dp);
-      vsm(u, s, dp, pf, sf);
-      m2(u, pf, sf);
+      if constexpr (D == 128) {
+        // one wave per SIMD: nothing else hides the transposed reads' LDS latency, so all of M2's A operands
+        // (2 x DT x 2 fragments, 64 VGPRs) are requested before the softmax VALU instead of just before their MFMAs
+        // (C4 dK/dV 46.8-47.1 -> 45.3-45.4 us, S 4096 166-170 -> 161-164; profiles/r04_ab_kv_m2pre_d128.jsonl)
+        const char* qs = smem + (unsigned)u * (unsigned)C::SLOT;
+        const char* dos = qs + C::QIMG;
+        f32x4 l2[4];
+        read_l2(u, l2);
+        bf16x8 od[2][DT], oq[2][DT];
+#pragma unroll
+        for (int st = 0; st < 2; ++st)
+#pragma unroll
+          for (int dt = 0; dt < DT; ++dt) {
+            od[st][dt] = tr_pair(dos + 16 * st * RB, tro[dt][0], tro[dt][1]);
+            oq[st][dt] = tr_pair(qs + 16 * st * RB, tro[dt][0], tro[dt][1]);
+          }
+        __builtin_amdgcn_sched_barrier(0);
+        vsm_l2(l2, s, dp, pf, sf);
+#pragma unroll
+        for (int st = 0; st < 2; ++st)
+#pragma unroll
+          for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+            for (int kt = 0; kt < KH; ++kt) {
+              dv[dt][kt] = mfma32(od[st][dt], pf[kt][st], dv[dt][kt]);
+              dk[dt][kt] = mfma32(oq[st][dt], sf[kt][st], dk[dt][kt]);
+            }
+      } else {
+        vsm(u, s, dp, pf, sf);
+        m2(u, pf, sf);
+      }
       q0cur = q0cur + QT >= qend ? qstart : q0cur + QT;
     }
   }
