@@ -22,6 +22,7 @@ Checks per rank: every parameter's main_grad (fp32) and .grad (bf16) equal the r
 (sum over the dp ranks' micro-batches of the unsplit model's gradient) / dp — within bf16 forward rounding;
 the dp replicas of a (pp, tp) position hold identical gradients (one all-reduce).
 """
+import json
 import os
 import socket
 
@@ -41,6 +42,11 @@ def _free_port():
     s.close()
     return p
 
+
+# relative L2 bound on every sharded gradient vs the unsplit HIP model's (bf16 activations, different
+# reduction orders under TP / PP / DP). Measured worst on MI355X: 1.04e-2 (c1_smollm_5l), 7.3e-3
+# (c4_llama2_7b_2l); the bound was 2.5e-2 until those were recorded ("loose").
+COMP_TOL = float(os.environ.get("PICO_COMP_TOL", "1.5e-2"))
 
 GEOMETRY = {
     # name: (config kwargs, mbs, seq, grad_acc)
@@ -227,7 +233,9 @@ def _worker(rank, world, port, geom, tp, pp, dp, out_dir):
         res[n] = (p.main_grad.detach().cpu().clone(), p.grad.detach().cpu().clone())
         assert torch.equal(p.grad, p.main_grad.to(bf)), n  # .grad = bf16 cast of the averaged main_grad
     torch.save(res, os.path.join(out_dir, f"pp{pp_rank}_tp{tr}_dp{m.dp_rank}.pt"))
-    bad = {k: v for k, v in errs.items() if not (v[0] < 2.5e-2 and v[1] < 2.5e-2)}
+    with open(os.path.join(out_dir, f"errs_pp{pp_rank}_tp{tr}_dp{m.dp_rank}.json"), "w") as f:
+        json.dump(errs, f)
+    bad = {k: v for k, v in errs.items() if not (v[0] < COMP_TOL and v[1] < COMP_TOL)}
     dist.barrier()
     dist.destroy_process_group()
     if bad:
@@ -239,6 +247,8 @@ def test_dp_tp_pp_1f1b_composition(geom, tp, pp, dp, tmp_path):
     world = tp * pp * dp
     mp.start_processes(_worker, args=(world, _free_port(), geom, tp, pp, dp, str(tmp_path)), nprocs=world,
                        join=True, start_method="spawn")
+    worst = max(max(v) for f in tmp_path.glob("errs_*.json") for v in json.load(open(f)).values())
+    print(f"[composition {geom}] worst gradient rel-L2 vs the unsplit model: {worst:.3e} (bound {COMP_TOL})")
     if dp > 1:
         for p in range(pp):
             for t in range(tp):
