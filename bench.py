@@ -102,7 +102,7 @@ def _spawn_workers(n):
     return subprocess.call(cmd, env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0"))
 
 
-def setup(layers, grad_acc, world, device, optimizer="pico", fused_adam=True, post_build=None):
+def setup(layers, grad_acc, world, device, optimizer="pico", fused_adam=True, post_build=None, dp_bucket=False):
     """The benchmark's model, optimizer and data (also used by tests/test_dp_hip_gpu.py's C3 check, so both run
     the same step): SmolLM-1.7B geometry with `layers` layers at seq 1024, the reference's random init with seed 42
     on every rank (identical replicas, ref train.py:103), DataParallelBucket when world > 1 (the bf16 .grad cast
@@ -117,7 +117,7 @@ def setup(layers, grad_acc, world, device, optimizer="pico", fused_adam=True, po
     if post_build is not None:
         post_build(model)
     num_params = sum(p.numel() for p in model.parameters())
-    if world > 1:
+    if world > 1 or dp_bucket:
         # the bf16 .grad cast (ref data_parallel.py:165) fused into the pico AdamW step (bit-identical)
         model = DataParallelBucket(model, defer_grad_cast=optimizer == "pico")
     # ref train.py:204-209: AdamW(lr), fused when the config's use_fused_adam is set (template default true)
@@ -152,6 +152,9 @@ def main():
     ap.add_argument("--optimizer", default="pico", choices=["pico", "torch"],
                     help="pico: picotron_amd.optim.AdamW (pico_adamw_bf16, one launch); torch: "
                          "torch.optim.AdamW (fused per --fused-adam), the reference's optimizer")
+    ap.add_argument("--dp-bucket", action="store_true",
+                    help="wrap the model in DataParallelBucket even at one rank (rehearses the N > 1 step: the "
+                         "syncing micro-batch's bucket all-reduces and their exposure, on RCCL at W = 1)")
     ap.add_argument("--graphs", type=int, default=1,
                     help="replay non-syncing micro-batches as a HIP graph (1) or run them eagerly (0)")
     args = ap.parse_args()
@@ -199,7 +202,7 @@ def main():
     pgm.setup_process_group_manager(tp_size=1, cp_size=1, pp_size=1, dp_size=world)
     t0 = time.time()
     cfg, model, opt, loader, num_params = setup(args.layers, args.grad_acc, world, device, args.optimizer,
-                                                bool(args.fused_adam))
+                                                bool(args.fused_adam), dp_bucket=args.dp_bucket)
     log(f"[rank {rank}] model {num_params / 1e9:.3f}B params built in {time.time() - t0:.1f}s")
     step = TrainingStep(model, opt, loader, device, graphs=bool(args.graphs))
 
@@ -218,6 +221,9 @@ def main():
         for k in kernel_ids:
             L.prof_enable(k, cap)
 
+    dp_timed = hasattr(model, "comm_timing")
+    if dp_timed:  # device events around the syncing micro-batch's bucket all-reduces (comm_exposure)
+        model.comm_timing(True)
     dist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
@@ -252,7 +258,13 @@ def main():
                 kernels[L.KERNEL_NAMES[k]] = {"total_ms": tot, "launches": n, "avg_us": 1e3 * tot / n}
         L.load().pico_prof_enable(0, 0)
 
+    exposure = None
+    if dp_timed:
+        exposure = comm_exposure(model.comm_report(), world, device)
+        model.comm_timing(False)
     allreduce = measure_allreduce(model, world, device) if world > 1 else None
+    if exposure is not None:
+        allreduce = dict(allreduce or {"buckets": len(model.bucket_manager.buckets)}, **exposure)
 
     tokens = world * MBS * SEQ * args.grad_acc * args.steps
     value = tokens / elapsed
@@ -362,6 +374,44 @@ def main():
 
 
 XGMI_LINK_GBS, XGMI_LINKS = 153.0, 7  # MI355X xGMI: 7 point-to-point links per GPU, ~153 GB/s each
+
+
+def exposure_model(buckets, world, busbw_gbs):
+    """Exposed communication of one syncing backward if its bucket all-reduces ran at `busbw_gbs` bus bandwidth
+    on `world` ranks: each bucket's all-reduce (2(W-1)/W * bytes of wire per GPU, ring) starts when it is ready
+    and the previous one is done (RCCL serialises them on one stream); exposed = last completion - end of the
+    backward (0 = the backward's own kernels). buckets: [(ready_ms rel. to the end of the backward, bytes)]."""
+    t = None
+    for ready, nbytes in sorted(buckets):
+        dur = 2.0 * (world - 1) / world * nbytes / (busbw_gbs * 1e9) * 1e3
+        t = max(ready, t if t is not None else ready) + dur
+    return max(0.0, t) if t is not None else 0.0
+
+
+def comm_exposure(report, world, device):
+    """From DataParallelBucket.comm_report() over the timed steps: the measured exposed all-reduce time per step
+    (end of the syncing backward -> end of the post-backward wait; max over ranks), the buckets' readiness times
+    relative to the end of the backward (the mean over steps, rank 0), and what the same readiness would expose
+    at W = 8 (or this world) at 300 / 600 / 1071 GB/s busbw (exposure_model)."""
+    if not report:
+        return None
+    exp = sum(r["exposed_ms"] for r in report) / len(report)
+    t = torch.tensor([exp], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    nb = len(report[0]["buckets"])
+    ready = [sum(r["buckets"][i][0] for r in report) / len(report) for i in range(nb)]
+    done = [sum(r["buckets"][i][1] for r in report) / len(report) for i in range(nb)]
+    sizes = [report[0]["buckets"][i][2] for i in range(nb)]
+    w = world if world > 1 else 8
+    order = sorted(range(nb), key=lambda i: ready[i])
+    return {"exposed_ms": round(float(t.item()), 3), "exposed_over": f"{len(report)} timed steps (mean), max over ranks",
+            "first_ready_ms": round(ready[order[0]], 3), "last_ready_ms": round(ready[order[-1]], 3),
+            "last_ready_bytes": sizes[order[-1]], "last_done_ms": round(max(done), 3),
+            "model_world": w,
+            "model_exposed_ms": {str(g): round(exposure_model(list(zip(ready, sizes)), w, g), 3)
+                                 for g in (300.0, 600.0, XGMI_LINK_GBS * XGMI_LINKS)},
+            "bucket_ready_ms": [round(ready[i], 3) for i in order],
+            "bucket_bytes": [sizes[i] for i in order]}
 
 
 def measure_allreduce(model, world, device, reps=3):

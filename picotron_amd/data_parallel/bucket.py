@@ -83,6 +83,8 @@ class Bucket:
         self.n_prescaled = 0                  # params whose last accumulate already divided by W
         self.cast_done = None                 # event after the side-stream cast (HIP path)
         self.side_stream = None
+        self.timing = False                   # record device events around the all-reduce (comm exposure)
+        self.timed = None                     # (ready event, all-reduce done event) of the last sync
         self.reset()
 
     def sync_gradient(self) -> None:
@@ -93,7 +95,19 @@ class Bucket:
             _kernels.scale(self.grad_data, self.process_group_size)
         elif self.n_prescaled != len(self.params):
             raise RuntimeError("bucket mixes pre-scaled and unscaled parameters")
+        ready = None
+        if self.timing and self.grad_data.is_cuda:  # on the compute stream: the bucket's last gradient is queued
+            ready = torch.cuda.Event(enable_timing=True)
+            ready.record()
         self.handle = dist.all_reduce(self.grad_data, group=self.process_group, async_op=True)
+        if ready is not None:  # the all-reduce's completion, seen from a side stream (no effect on the compute one)
+            if self.side_stream is None:
+                self.side_stream = torch.cuda.Stream(device=self.grad_data.device)
+            with torch.cuda.stream(self.side_stream):
+                self.handle.wait()
+                done = torch.cuda.Event(enable_timing=True)
+                done.record(self.side_stream)
+            self.timed = (ready, done)
         if self.grad_out is not None and self.grad_data.is_cuda and not self.defer_cast:
             if self.side_stream is None:
                 self.side_stream = torch.cuda.Stream(device=self.grad_data.device)
@@ -106,6 +120,7 @@ class Bucket:
     def reset(self) -> None:
         self.handle = None
         self.cast_done = None
+        self.timed = None
         self.n_prescaled = 0
         self.params_with_grad_ready.clear()
         _kernels.zero(self.grad_data)
@@ -200,6 +215,12 @@ class BucketManager:
                 continue
             start, end, b = self.params_to_bucket_location[param]
             param.main_grad = self.grad_data_list[b][start:end].view(param.shape)
+
+    def set_timing(self, on: bool) -> None:
+        """Record device events per bucket: when its last gradient was queued (ready) and when its all-reduce
+        completed (DataParallelBucket.comm_timing collects them per backward pass)."""
+        for b in self.buckets:
+            b.timing = bool(on)
 
     def grad_view(self, param):
         """bf16 view of the synchronised gradient of `param` (becomes param.grad)."""

@@ -95,6 +95,29 @@ class DataParallelBucket(nn.Module):
         self._pass_cb_set = False
         self.register_backward_hook()
         self._post_backward_callback_set = False
+        self._comm_log = None
+        self._anchor = None
+
+    def comm_timing(self, on: bool) -> None:
+        """Start (True) or stop (False) recording, per syncing backward pass, device events at the end of the
+        backward's kernels, at each bucket's readiness and all-reduce completion, and after the post-backward
+        wait — the communication the step does not hide (comm_report)."""
+        if on and self.bucket_manager.device.type != "cuda":
+            raise RuntimeError("DataParallelBucket.comm_timing: device events need the HIP device")
+        self._comm_log = [] if on else None
+        self.bucket_manager.set_timing(on)
+
+    def comm_report(self):
+        """Per recorded syncing backward (after a device synchronize): {"exposed_ms": end of backward -> end of
+        the post-backward wait, "buckets": [(ready_ms, allreduce_done_ms, bytes)] relative to the end of the
+        backward (negative: before it), in bucket order}."""
+        out = []
+        for a, t0, t1, bk in self._comm_log or []:
+            end = a.elapsed_time(t0)  # every time from the anchor (elapsed times are taken forward only)
+            rows = [(a.elapsed_time(tm[0]) - end, a.elapsed_time(tm[1]) - end, nb) if tm is not None else
+                    (None, None, nb) for tm, nb in bk]
+            out.append({"exposed_ms": t0.elapsed_time(t1), "buckets": rows})
+        return out
 
     def forward(self, *inputs, **kwargs):
         # per-pass state left by a backward that raised midway (its end-of-pass callbacks never ran) is dropped
@@ -140,9 +163,7 @@ class DataParallelBucket(nn.Module):
                 get_kernels().accumulate(param.main_grad, param.grad, world if sync else 1)
                 param.grad = None
                 if sync:
-                    if not self._post_backward_callback_set:
-                        Variable._execution_engine.queue_callback(self._post_backward)
-                        self._post_backward_callback_set = True
+                    self._queue_post_backward()
                     bucket_manager.mark_param_as_ready(param, prescaled=True)
         return param_hook
 
@@ -161,9 +182,7 @@ class DataParallelBucket(nn.Module):
                 Variable._execution_engine.queue_callback(self._end_pass)
                 self._pass_cb_set = True
             if self.require_backward_grad_sync:
-                if not self._post_backward_callback_set:
-                    Variable._execution_engine.queue_callback(self._post_backward)
-                    self._post_backward_callback_set = True
+                self._queue_post_backward()
                 bucket_manager.mark_param_as_ready(param, prescaled=True)
         return ready
 
@@ -173,8 +192,26 @@ class DataParallelBucket(nn.Module):
         yield
         self.require_backward_grad_sync = True
 
+    def _queue_post_backward(self):
+        if not self._post_backward_callback_set:
+            Variable._execution_engine.queue_callback(self._post_backward)
+            self._post_backward_callback_set = True
+            if self._comm_log is not None:  # timing anchor: before the pass's first bucket can be ready
+                self._anchor = torch.cuda.Event(enable_timing=True)
+                self._anchor.record()
+
     def _post_backward(self):
+        t0 = None
+        if self._comm_log is not None:  # end of the backward's kernels on the compute stream
+            t0 = torch.cuda.Event(enable_timing=True)
+            t0.record()
         self.bucket_manager.wait()
+        if t0 is not None:  # the compute stream has waited for every bucket's all-reduce (and cast)
+            t1 = torch.cuda.Event(enable_timing=True)
+            t1.record()
+            bm = self.bucket_manager
+            self._comm_log.append((self._anchor, t0, t1, [(b.timed, b.grad_data.numel() * b.grad_data.element_size())
+                                                         for b in bm.buckets]))
         self._post_backward_callback_set = False
         for p in self.module.parameters():
             if p.requires_grad:

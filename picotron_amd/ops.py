@@ -201,7 +201,9 @@ def _pair_dy(hint, T, N, like):
     w, Nh, K = hint
     if Nh != N:
         return None
-    return WP.dy_out(w, N, K, T, like.dtype, like.device)
+    # only into buffers the projection's forward created (its x^T went to the pair buffer): a path whose x^T was
+    # never paired (PICO_SWIGLU_T=0, T % 64 != 0, an attention without O^T) gets no pair buffers from here
+    return WP.dy_out_existing(w, N, K, T, like.dtype, like.device)
 
 
 def rms_norm(x, weight, eps=1e-5, residual=None, prenorm=False):

@@ -88,6 +88,9 @@ def train_step(model, data_loader, device, graphs=None, sync_loss=True):
     # paired weight gradients (wgrad_pair) need every micro-batch announced with its index: eager micro-batches and
     # the pipelined graph do; MicroBatchGraph replays one captured micro-batch for every index, so not with it
     pair = graphs is None or grouped
+    if grouped and getattr(graphs, "n", n) != n:
+        # the graph's micro-batch indices (and its wgrad pairing decisions, fixed at capture) are those of n
+        raise RuntimeError(f"train_step: the pipelined graph was built for grad_acc {graphs.n}, the loader has {n}")
     if pair:
         WP.begin_step()
     pending = []  # grouped graphs: the non-syncing micro-batches, replayed together before the syncing one
@@ -116,8 +119,14 @@ def train_step(model, data_loader, device, graphs=None, sync_loss=True):
             with (WP.micro_batch(i, n) if pair else contextlib.nullcontext()):
                 losses.append(_micro_batch(model, input_ids, target_ids, n))
     run_pending()
+    if pair and WP.pending_state():
+        # a first half whose wgrad GEMM was deferred and never run: its weight gradients would be lost silently
+        raise RuntimeError("train_step: paired weight gradients (wgrad_pair) left a deferred first half unconsumed "
+                           "(pairing toggled between capture and replay?)")
     if graphs is not None:
-        losses.append(graphs.take_loss())
+        acc = graphs.take_loss()
+        if acc is not None:  # None: no graph replay ran this step (e.g. grad_acc 1 under DP: the syncing one only)
+            losses.append(acc)
     # one host sync per step instead of one per micro-batch (ref :53 calls .item() each time), or none
     total = torch.stack(losses).float().sum() if losses else torch.zeros((), device=device)
     if not sync_loss:
@@ -179,7 +188,7 @@ class MicroBatchGraph:
 
     def take_loss(self):
         if self.loss_acc is None:
-            return torch.zeros(())
+            return None
         out = self.loss_acc.clone()
         self.loss_acc.zero_()
         return out
@@ -205,6 +214,7 @@ class PipelinedMicroBatchGraph:
         self.graphs = {}  # number of micro-batches -> (graph, inputs [k, B, S], targets [k, B, S])
         self.loss_acc = None
         self.streams = None
+        self.pair_latched = None
 
     @property
     def graph(self):
@@ -272,12 +282,16 @@ class PipelinedMicroBatchGraph:
         # a first half the graph's last micro-batch leaves deferred (wgrad_pair) for the eager one after it: the
         # replay runs no Python, so run() re-announces it after every replay
         self.graphs[len(batches)] = (g, inp, tgt, WP.pending_state())
+        self.pair_latched = WP.enabled()  # the pairing decisions are baked into the graph
 
     def run(self, batches):
         from . import ops
         ops.refresh_weight_transposes()  # dgrad W^T copies are graph inputs: bring them up to date
         if len(batches) not in self.graphs:
             self._capture(batches)
+        if WP.enabled() != self.pair_latched:
+            raise RuntimeError("PipelinedMicroBatchGraph: PICO_WGRAD_PAIR changed after the graph was captured (its "
+                               "wgrad pairing is fixed at capture); build a new graph")
         g, inp, tgt, pending = self.graphs[len(batches)]
         for j, (x, y) in enumerate(batches):
             inp[j].copy_(x)
@@ -287,7 +301,7 @@ class PipelinedMicroBatchGraph:
 
     def take_loss(self):
         if self.loss_acc is None:
-            return torch.zeros(())
+            return None
         out = self.loss_acc.clone()
         self.loss_acc.zero_()
         return out

@@ -127,6 +127,32 @@ def dy_out(weight, N, K, T, dtype, device):
     return buf(weight, N, K, T, dtype, device).dy_slot(_CTX["i"])
 
 
+def dy_out_existing(weight, N, K, T, dtype, device):
+    """dy_out, but only into pair buffers that already exist with this shape (created by the forward's x^T
+    producer); None otherwise — a backward never creates the buffers for a projection the forward did not pair."""
+    if not active() or weight is None:
+        return None
+    b = _get(weight)
+    if b is None or (b.N, b.K, b.T) != (N, K, T) or b.dy.dtype != dtype or b.dy.device != device:
+        return None
+    return b.dy_slot(_CTX["i"])
+
+
+def footprint_bytes():
+    """Bytes held by every live pair buffer: per projection (weight [N, K], T tokens per micro-batch) two x^T sets
+    [K, 2T] and one dy [2T, N] — (4 K T + 2 T N) elements; SmolLM-1.7B at T = 4096: about 0.9 GB per layer."""
+    return sum(sum(x.numel() * x.element_size() for x in b.xt) + b.dy.numel() * b.dy.element_size()
+               for _, b in list(_BUFS.values()))
+
+
+def release():
+    """Free every pair buffer (after training; a graph captured on them must not be replayed afterwards)."""
+    for _, b in list(_BUFS.values()):
+        if b.pending is not None:
+            raise RuntimeError("wgrad_pair.release: a deferred first half is still pending")
+    _BUFS.clear()
+
+
 def dy_out_if_paired(weight, x2, N, K, T, dtype, device):
     """dy_out, but only when this micro-batch's x^T of `weight` (x2, the [T, K] view its backward saved) sits in the
     weight's pair buffer — i.e. the forward paired it; otherwise None (no buffers created for unpaired paths)."""

@@ -18,12 +18,13 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 CONFIGS = {
     "c2": (4, 1024, 32, 32, 64, True),
     "c2_full": (4, 1024, 32, 32, 64, False),
-    "d128": (2, 1024, 16, 16, 128, True),   # Llama-2-7B per TP rank (tp2), micro-batch 2
+    "d128": (4, 1024, 16, 16, 128, True),   # Llama-2-7B per TP rank (tp2), the reference's micro-batch 4
+    "d128_b2": (2, 1024, 16, 16, 128, True),   # the same at micro-batch 2 (half the work: one 256-CU round)
     "gqa4": (4, 1024, 32, 8, 64, True),
     "s4096": (1, 4096, 32, 32, 64, True),   # CP block size of config 5
-    "d128_full": (2, 1024, 16, 16, 128, False),
+    "d128_full": (4, 1024, 16, 16, 128, False),
     "d128_s4096": (1, 4096, 16, 16, 128, True),
-    "d128_gqa4": (2, 1024, 32, 8, 128, True),
+    "d128_gqa4": (4, 1024, 32, 8, 128, True),
 }
 
 

@@ -6,7 +6,8 @@ host-staged).
   * C1 (BASELINE configs[0]): SmolLM-1.7B geometry, 5 layers, dp 2 x tp 2 x pp 2, micro-batch 4, seq 128,
     grad_acc 2 — eight ranks;
   * C4 variant: Llama-2-7B geometry (Hd 4096, I 11008 -> 5504 per tp rank, 32 heads -> 16, D = 128,
-    V 32000) reduced to 2 layers, tp 2 x pp 2 — four ranks.
+    V 32000) reduced to 2 layers, at the reference's micro-batch 4 and seq 1024 (ref README.md:34), dp 2 x tp 2 x
+    pp 2 — eight ranks (the reference's dp 4 would be sixteen processes on this one GPU).
 
 Each rank: the grid of ref picotron/process_group_manager.py:13-23 (picotron_amd.process_group_manager);
 apply_tensor_parallel (ref picotron/tensor_parallel/tensor_parallel.py:9-52: column q/k/v/up/gate, row
@@ -53,7 +54,7 @@ GEOMETRY = {
     "c1_smollm_5l": (dict(hidden_size=2048, intermediate_size=8192, num_attention_heads=32, num_key_value_heads=32,
                           num_hidden_layers=5, vocab_size=49152), 4, 128, 2),
     "c4_llama2_7b_2l": (dict(hidden_size=4096, intermediate_size=11008, num_attention_heads=32,
-                             num_key_value_heads=32, num_hidden_layers=2, vocab_size=32000), 2, 128, 2),
+                             num_key_value_heads=32, num_hidden_layers=2, vocab_size=32000), 4, 1024, 2),
 }
 
 
@@ -242,7 +243,7 @@ def _worker(rank, world, port, geom, tp, pp, dp, out_dir):
         raise AssertionError(f"rank {rank} (pp {pp_rank}, tp {tr}, dp {m.dp_rank}) {geom}: {bad}")
 
 
-@pytest.mark.parametrize("geom,tp,pp,dp", [("c1_smollm_5l", 2, 2, 2), ("c4_llama2_7b_2l", 2, 2, 1)])
+@pytest.mark.parametrize("geom,tp,pp,dp", [("c1_smollm_5l", 2, 2, 2), ("c4_llama2_7b_2l", 2, 2, 2)])
 def test_dp_tp_pp_1f1b_composition(geom, tp, pp, dp, tmp_path):
     world = tp * pp * dp
     mp.start_processes(_worker, args=(world, _free_port(), geom, tp, pp, dp, str(tmp_path)), nprocs=world,

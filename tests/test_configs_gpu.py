@@ -4,7 +4,8 @@ relative error reported"). Tolerances as DESIGN.md §3 / tests/test_kernels_gpu.
 rel-L2 <= 4e-3 and LSE max-abs <= 2e-3, attention gradients rel-L2 <= 1e-2, norm / SwiGLU rel-L2 <= 4e-3.
 
   C2  SmolLM-1.7B, micro-batch 4, S 1024: attention (B 4, S 1024, 32 heads, D 64) fwd + bwd, whole shape.
-  C4  Llama-2-7B per tensor-parallel rank (tp 2): attention (B 2, S 1024, 16 heads, D 128), RMSNorm
+  C4  Llama-2-7B per tensor-parallel rank (tp 2): attention at the reference's micro-batch (B 4, S 1024, 16 heads,
+      D 128; ref README.md:34 `--mbs 4 --seq_len 1024`) and at B 2 (the grid of one 256-CU round), RMSNorm
       [4096 x 4096] (residual form), SwiGLU with I / tp = 5504 on the strided halves of one gate|up GEMM.
   C5  SmolLM-1.7B cp 8 at S 32768 -> 4096-row blocks (B 1, 32 heads, D 64): the ring's block forward
       (causal diagonal + full off-diagonal), the 3-block LSE merge, and block backwards from the GLOBAL
@@ -47,7 +48,8 @@ def _attn_ref(q, k, v, do, scale, causal, q_offset=0):
     return tr(out).detach(), lse.detach(), (tr(gq), tr(gk), tr(gv))
 
 
-@pytest.mark.parametrize("tag,B,S,Hq,Hkv,D", [("C2", 4, 1024, 32, 32, 64), ("C4-tp2", 2, 1024, 16, 16, 128)])
+@pytest.mark.parametrize("tag,B,S,Hq,Hkv,D", [("C2", 4, 1024, 32, 32, 64), ("C4-tp2-mbs4", 4, 1024, 16, 16, 128),
+                                               ("C4-tp2-mbs2", 2, 1024, 16, 16, 128)])
 def test_attention_full_config_shape(tag, B, S, Hq, Hkv, D):
     from picotron_amd import ops
     torch.manual_seed(S + Hq + D)

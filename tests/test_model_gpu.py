@@ -62,13 +62,39 @@ def _loss_curve(model, golden_loss, steps, fused=False):
     return losses
 
 
+def _bf16_ulp(x):
+    """One bf16 ulp at |x| (8 significant bits): the resolution of the reference's recorded loss values."""
+    return 2.0 ** (math.floor(math.log2(abs(x))) - 7)
+
+
+# Overlay band (SURVEY §8c; VERDICT r04 "What's weak" 1b), in the reference's own resolution: the reference's
+# losses are bf16 values, so from step 10 on every step must lie within OVERLAY_ULPS bf16 ulps of the
+# reference's value plus an absolute OVERLAY_FLOOR for the low-loss tail (below loss 1 an ulp is < 0.004, while
+# two bf16 training runs whose GEMMs sum in different orders drift by ~0.005 there: r01's eager curve peaks at
+# 3.7 ulps = 0.007 at loss 0.30, step 148); and the mean |dloss| over steps 10-199 <= OVERLAY_MEAN.
+OVERLAY_ULPS, OVERLAY_FLOOR, OVERLAY_MEAN = 2.0, 0.01, 0.015
+
+
+def _assert_overlay(losses, ref, tag):
+    diffs = [abs(a - b) for a, b in zip(losses, ref)]
+    ulps = [diffs[i] / _bf16_ulp(ref[i]) for i in range(200)]
+    worst = max(range(10, 200), key=lambda i: diffs[i] / (OVERLAY_ULPS * _bf16_ulp(ref[i]) + OVERLAY_FLOOR))
+    mean = sum(diffs[10:200]) / 190
+    print(f"[loss-overlay] {tag}: max |dloss| {max(diffs[10:200]):.4f}, max {max(ulps[10:200]):.2f} bf16 ulps, "
+          f"tightest step {worst} (|d| {diffs[worst]:.4f} at loss {ref[worst]:.4f} = {ulps[worst]:.2f} ulps), "
+          f"mean |dloss| steps 10-199 {mean:.4f}", flush=True)
+    for i in range(10, 200):
+        assert diffs[i] <= OVERLAY_ULPS * _bf16_ulp(ref[i]) + OVERLAY_FLOOR, (i, losses[i], ref[i], ulps[i])
+    assert mean <= OVERLAY_MEAN, mean
+
+
 def test_loss_curve_overlays_reference(golden_loss):
     """200 steps with bf16 params + bf16 AdamW states (the reference's GPU dtype policy, ref
     train.py:76,190) against the reference's own run of the same init/data in that dtype policy
     (its eager path on CPU, `losses_bf16`). Tolerance: step 0 == ln V to 1e-3 (zero LM head);
-    after step 10 |dloss| <= 0.06 + 3 % of the reference loss (the reference's loss values are
-    bf16-rounded: 1 ulp = 0.8 %); mean |dloss| <= 0.02. Against the fp32 curve the bf16 policy
-    itself lags by up to ~0.25 (recorded, loosely bounded)."""
+    after step 10 |dloss| <= 2 bf16 ulps of the reference's loss + 0.01, mean |dloss| over steps 10-199
+    <= 0.015 (_assert_overlay). Against the fp32 curve the bf16 policy itself lags by up to ~0.25
+    (recorded, loosely bounded)."""
     from picotron_amd.model import build_llama
     torch.manual_seed(golden_loss["seed"])
     m = build_llama(_cfg(golden_loss), device="cuda", dtype=BF)
@@ -81,10 +107,7 @@ def test_loss_curve_overlays_reference(golden_loss):
         with open(out, "w") as f:
             json.dump({"gpu_bf16": losses, "reference_cpu_bf16": ref, "reference_cpu_fp32": ref32}, f)
     assert abs(losses[0] - math.log(golden_loss["config"]["vocab_size"])) < 1e-3
-    diffs = [abs(a - b) for a, b in zip(losses, ref)]
-    for i in range(10, 200):
-        assert diffs[i] <= 0.06 + 0.03 * ref[i], (i, losses[i], ref[i])
-    assert sum(diffs) / len(diffs) <= 0.02
+    _assert_overlay(losses, ref, "eager layers")
     assert sum(abs(a - b) for a, b in zip(losses, ref32)) / 200 <= 0.25
 
 
@@ -139,10 +162,7 @@ def test_loss_curve_shipped_path_overlays_reference(golden_loss, kind):
     # step 0 = ln V up to the bf16 rounding of each micro-batch's loss (the fused CE returns the loss in the
     # logits' dtype, as ATen's does: ln 512 / 2 lies in [2, 4), 1 bf16 ulp = 0.0156)
     assert abs(losses[0] - math.log(cfg["vocab_size"])) <= 0.02
-    diffs = [abs(a - b) for a, b in zip(losses, ref)]
-    for i in range(10, 200):
-        assert diffs[i] <= 0.06 + 0.03 * ref[i], (i, losses[i], ref[i])
-    assert sum(diffs) / len(diffs) <= 0.02
+    _assert_overlay(losses, ref, f"shipped {kind}")
 
 
 def test_dp_bucket_rccl_world1(golden_loss, monkeypatch):
@@ -247,7 +267,7 @@ _PAIR_CFG = dict(hidden_size=1024, intermediate_size=2048, num_attention_heads=1
 
 
 @pytest.mark.parametrize("n,dp,graph", [(4, False, False), (3, False, False), (4, True, False), (4, False, True),
-                                        (3, True, True)])
+                                        (3, True, True), (4, True, True)])
 def test_wgrad_pairs_match_unpaired(monkeypatch, n, dp, graph):
     """Paired weight gradients (wgrad_pair: two micro-batches' wgrad GEMMs as one over both, the producers writing
     x^T / dy straight into the pair buffers) == the unpaired loop (PICO_WGRAD_PAIR=0): the loss bit for bit (the
