@@ -28,6 +28,7 @@
 // one lane (accumulator tiles dt and dt + D/64), so it is register-local.
 #include "attn_common.h"
 
+#include <algorithm>
 #include <type_traits>
 
 
@@ -86,6 +87,32 @@ struct KVCfg {
   static constexpr int NP = 2 * NQP + 1;
   static constexpr int NPW = (NP + KNW - 1) / KNW;
 };
+
+// One-round causal schedule of the dK/dV kernel (round 5). A causal grid of one workgroup per 128-key block has
+// blocks of unequal work (C2: 32, 28, ..., 4 query tiles per key block) and, at three workgroups per CU, 1024
+// workgroups for 768 slots: the light blocks that do not fit the first round ran as a tail in a near-empty chip
+// (blocks 6-7 from 39 to 52 us, one slot in three busy; profiles/r03_attn_wg_timelines.json). Grouped, each
+// workgroup runs a short list of key blocks of one (batch, kv-head) one after the other, sized so that every
+// head's groups fill exactly one round: with the CU's SIMD arbitration by age (the oldest of three resident
+// workgroups runs a tile in ~1.15 us, the youngest in ~2.2), the groups dispatched first get the most work (host:
+// block_groups). Same box, 3 interleaved rounds (profiles/r05_ab_attn_groups.jsonl): C2 dK/dV 57.4 -> 56.3 us,
+// C4 (B 4, D 128, one workgroup per CU: 512 blocks -> 256 groups of equal work) 59.3 -> 58.4; the same grouping of
+// the dQ kernel's query blocks measured slower (C2 42.8 -> 47.3 us, GQA-4 40.0 -> 43.9: its lightest-first front,
+// q_front, frees slots early for the heavy blocks, which a one-round grid cannot), so the dQ grid stays plain.
+// grp.n == 0: the plain grid, one block per workgroup.
+struct BlkGroups {
+  int n;          // groups per (batch, head); 0 = one block per workgroup
+  unsigned cnt;   // blocks in group g: nibble g (1..4)
+  unsigned w[8];  // block ids of group g: byte j of w[g], j < its count (heaviest first)
+};
+
+// w[g] for a wave-uniform g without indexing the kernel-argument array (selects, no scratch copy)
+PICO_DEV unsigned grp_sel(const BlkGroups& t, int g) {
+  unsigned r = t.w[0];
+#pragma unroll
+  for (int i = 1; i < 8; ++i) r = g == i ? t.w[i] : r;
+  return r;
+}
 
 PICO_DEV float halves_sum2(float x) {
   const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
@@ -354,20 +381,21 @@ __global__ __launch_bounds__(256, QCfg<D>::MINB) void attn_bwd_q_kernel(const pi
       }
   }
   if (a.flags & PICO_ATTN_DQ_F32_ACCUM) {
-    if (!row_ok) return;
-    float* dst = (float*)a.dq + b * a.dq_strides[0] + hq * a.dq_strides[2] + (int64_t)my_q * a.dq_strides[1];
+    if (row_ok) {
+      float* dst = (float*)a.dq + b * a.dq_strides[0] + hq * a.dq_strides[2] + (int64_t)my_q * a.dq_strides[1];
 #pragma unroll
-    for (int dt = 0; dt < DT; ++dt)
+      for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        float* p = dst + 32 * dt + 8 * g + 4 * h;
+        for (int g = 0; g < 4; ++g) {
+          float* p = dst + 32 * dt + 8 * g + 4 * h;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) p[j] += dq[dt][4 * g + j] * scale;
-      }
-    return;
+          for (int j = 0; j < 4; ++j) p[j] += dq[dt][4 * g + j] * scale;
+        }
+    }
+  } else {
+    bf16_t* dst = (bf16_t*)a.dq + b * a.dq_strides[0] + hq * a.dq_strides[2] + (int64_t)qc * a.dq_strides[1];
+    store_row_bf16_x16<DT>(dst, h, row_ok, [&](int dt, int i) { return dq[dt][i] * scale; });
   }
-  bf16_t* dst = (bf16_t*)a.dq + b * a.dq_strides[0] + hq * a.dq_strides[2] + (int64_t)qc * a.dq_strides[1];
-  store_row_bf16_x16<DT>(dst, h, row_ok, [&](int dt, int i) { return dq[dt][i] * scale; });
 #if PICO_BWDQ_WGSTAMP
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -385,14 +413,14 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kv_kernel(const pico_
                                                               const float* __restrict__ lse2_g,
                                                               const float* __restrict__ delta_g, int sq_pad,
                                                               int hsplit, float* __restrict__ dkv_part,
-                                                              unsigned long long* __restrict__ stamp_out) {
+                                                              unsigned long long* __restrict__ stamp_out,
+                                                              const BlkGroups grp) {
   using C = KVCfg<D>;
   constexpr int KS = C::KS, DT = C::DT, CPR = C::CPR, RB = C::RB;
   __shared__ __attribute__((aligned(16))) char smem[C::NBUF * C::SLOT];
 
-  const int lane = threadIdx.x & 63;
+  const int lane0 = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int r = lane & 31, h = lane >> 5;
   const int Sq = (int)a.seqlen_q, Sk = (int)a.seqlen_k;
   const int Hq = (int)a.heads_q;
   const int G = (int)(a.heads_q / a.heads_kv);
@@ -405,11 +433,23 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kv_kernel(const pico_
   // measured neutral here); small grids split a key block's (query head, query tile) list over `hsplit`
   // workgroups with fp32 partials (attn_bwd_dkv_kernel sums)
   const int nbh = (int)(a.batch * a.heads_kv) * hsplit;
-  const int kb = blockIdx.x / nbh;
+  const int gi = blockIdx.x / nbh;  // the key block, or with a one-round schedule (grp.n > 0) the block group
   const int bhs = blockIdx.x % nbh;
   const int hs = bhs % hsplit;
   const int bh = bhs / hsplit;
   const int b = bh / (int)a.heads_kv, hk = bh % (int)a.heads_kv;
+  // the group's key blocks one after the other (grp.n == 0: the one block gi)
+  const unsigned gw = grp.n ? grp_sel(grp, gi) : 0u;
+  const int nblk_wg = grp.n ? (int)((grp.cnt >> (4 * gi)) & 15u) : 1;
+#pragma clang loop unroll(disable)
+  for (int jb = 0; jb < nblk_wg; ++jb) {
+  const int kb = grp.n ? (int)((gw >> (8 * jb)) & 255u) : gi;
+  if (jb > 0) lds_barrier();  // every wave is done with the ring before this block's prologue DMA refills it
+  // the lane id through an opaque copy: nothing lane-dependent is hoisted out of the block loop and kept live
+  // across the whole body (that cost 100-180 B of scratch per lane at these register budgets)
+  int lane_l = lane0;
+  asm volatile("" : "+v"(lane_l));
+  const int lane = lane_l, r = lane & 31, h = lane >> 5;
   const int k0 = kb * KVB;
   const int kw = k0 + KPW * wave;  // this wave's first key
 
@@ -495,7 +535,11 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kv_kernel(const pico_
         // id here instead of being held in a VGPR for the whole sweep — at 168 VGPRs that VGPR was spilled, and
         // its scratch reload's vmcnt(0) drained wave 0's whole DMA queue (two tiles of prefetch) every tile
         static_assert(C::NP % KNW == 1 && C::NP / KNW == C::NPW - 1, "the LSE / delta piece is wave 0's last");
-        const int l = (int)__lane_id() & 15;
+        // (from an opaque copy of the lane id: a plain __lane_id() expression is loop-invariant and gets hoisted
+        // out of the tile loop into that same long-lived, spilled VGPR)
+        int l = lane0;
+        asm volatile("" : "+v"(l));
+        l &= 15;
         dma_piece(c.p[i], (unsigned)(16 * (l & 7)) + ((l >> 3) ? delta_off : 0u), dst + pc_dst[i]);
       }
     }
@@ -775,6 +819,7 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kv_kernel(const pico_
         }
     }
   }
+  }  // key blocks of the group
 #if PICO_BWDKV_WGSTAMP
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   wgs[3] = __builtin_amdgcn_s_memrealtime();
@@ -826,6 +871,69 @@ int q_front(const pico_attn_args* a) {
   return first < nmb ? (int)(nmb - first) : 0;
 }
 
+// PICO_ATTN_GROUPS=0 restores the plain causal grids (one block per workgroup; A/B switch)
+bool groups_enabled() {
+  const char* e = getenv("PICO_ATTN_GROUPS");
+  return !(e && e[0] == '0');
+}
+
+// The one-round schedule of BlkGroups: the nblk blocks of each (batch, head) (work wt[i] in tiles) cut into
+// G = minb * CUs / nbh groups, so that the grid is exactly one round of minb workgroups per CU. Groups are
+// dispatched g-major, so a group's place among a CU's resident workgroups (oldest first) is g * nbh / CUs; its
+// target work is proportional to the tile rate of that place (measured at three per CU, C2 dK/dV: 1.15 / 1.53 /
+// 2.2 us per tile -> 1 / 0.75 / 0.53). Blocks go heaviest first to the group with the most target left (at most
+// 4 per group). n = 0 (the plain grid) when that grid is one round already or the cut does not fit the table.
+BlkGroups block_groups(const int* wt, int nblk, int64_t nbh, int minb) {
+  BlkGroups t{};
+  const int cus = pico_num_cus();
+  const int64_t slots = (int64_t)minb * cus;
+  if (!groups_enabled() || nbh <= 0 || nblk > 32 || (int64_t)nblk * nbh <= slots) return t;
+  const int G = (int)(slots / nbh);
+  if (G < 2 || G > 8 || nblk > 4 * G) return t;
+  static const double spd[3] = {1.0, 0.75, 0.53};
+  double tgt[8], load[8] = {0.0}, tot = 0.0, ssum = 0.0;
+  int cnt[8] = {0};
+  for (int i = 0; i < nblk; ++i) tot += wt[i];
+  for (int g = 0; g < G; ++g) {
+    const int cls = (int)std::min<int64_t>(minb - 1, (int64_t)g * nbh / cus);
+    tgt[g] = minb == 1 ? 1.0 : spd[std::min(cls, 2)];
+    ssum += tgt[g];
+  }
+  for (int g = 0; g < G; ++g) tgt[g] *= tot / ssum;
+  int order[32];
+  for (int i = 0; i < nblk; ++i) order[i] = i;
+  std::stable_sort(order, order + nblk, [&](int x, int y) { return wt[x] > wt[y]; });
+  for (int k = 0; k < nblk; ++k) {
+    const int i = order[k];
+    int best = -1;
+    for (int g = 0; g < G; ++g)
+      if (cnt[g] < 4 && (best < 0 || tgt[g] - load[g] > tgt[best] - load[best])) best = g;
+    if (best < 0) return BlkGroups{};
+    t.w[best] |= (unsigned)i << (8 * cnt[best]);
+    ++cnt[best];
+    load[best] += wt[i];
+  }
+  for (int g = 0; g < G; ++g) {
+    if (cnt[g] == 0) return BlkGroups{};
+    t.cnt |= (unsigned)cnt[g] << (4 * g);
+  }
+  t.n = G;
+  return t;
+}
+
+// dK/dV kernel groups: key block kb sees (Hq / Hkv) * ceil((Sq - 128 kb) / 32) query tiles (causal, no hsplit)
+BlkGroups kv_groups(const pico_attn_args* a, int hsplit, int minb) {
+  if (!a->causal || hsplit != 1 || a->heads_kv <= 0) return BlkGroups{};
+  const int nkb = (int)((a->seqlen_k + KVB - 1) / KVB);
+  if (nkb > 32) return BlkGroups{};
+  int wt[32];
+  for (int kb = 0; kb < nkb; ++kb) {
+    const int64_t q0 = (int64_t)kb * KVB;
+    wt[kb] = (int)((a->heads_q / a->heads_kv) * (a->seqlen_q > q0 ? (a->seqlen_q - q0 + QT - 1) / QT : 0));
+  }
+  return block_groups(wt, nkb, a->batch * a->heads_kv, minb);
+}
+
 template <int D, bool CAUSAL>
 int launch_split(const pico_attn_args* a, hipStream_t s) {
   const int sq_pad = split_sq_pad(a);
@@ -842,18 +950,19 @@ int launch_split(const pico_attn_args* a, hipStream_t s) {
                        q_front(a)));
   const int nkb = (int)((a->seqlen_k + KVB - 1) / KVB);
   const int hsplit = kv_hsplit(a);
-  const int64_t nblk = (int64_t)nkb * a->batch * a->heads_kv * hsplit;
+  const BlkGroups kg = kv_groups(a, hsplit, kv_minb(a));
+  const int64_t nblk = (int64_t)(kg.n ? kg.n : nkb) * a->batch * a->heads_kv * hsplit;
   if (nblk == 0) return 0;
   unsigned long long* stamps = (unsigned long long*)((char*)a->workspace + pico_attn_bwd_split_workspace(a) - STAMP_BYTES);
   if constexpr (D == 128) {
     PICO_TRY(pico_launch(PICO_K_ATTN_BWD_KV, "attn_bwd_kv", attn_bwd_kv_kernel<D, CAUSAL, 1>, dim3((int)nblk),
-                         dim3(KNW * 64), 0, s, *a, a->softmax_scale, sl2, lse2, delta, sq_pad, hsplit, dkv_part, stamps));
+                         dim3(KNW * 64), 0, s, *a, a->softmax_scale, sl2, lse2, delta, sq_pad, hsplit, dkv_part, stamps, kg));
   } else if constexpr (CAUSAL) {
     PICO_TRY(pico_launch(PICO_K_ATTN_BWD_KV, "attn_bwd_kv", attn_bwd_kv_kernel<D, CAUSAL, 3>, dim3((int)nblk),
-                         dim3(KNW * 64), 0, s, *a, a->softmax_scale, sl2, lse2, delta, sq_pad, hsplit, dkv_part, stamps));
+                         dim3(KNW * 64), 0, s, *a, a->softmax_scale, sl2, lse2, delta, sq_pad, hsplit, dkv_part, stamps, kg));
   } else {
     PICO_TRY(pico_launch(PICO_K_ATTN_BWD_KV, "attn_bwd_kv", attn_bwd_kv_kernel<D, CAUSAL, 2>, dim3((int)nblk),
-                         dim3(KNW * 64), 0, s, *a, a->softmax_scale, sl2, lse2, delta, sq_pad, hsplit, dkv_part, stamps));
+                         dim3(KNW * 64), 0, s, *a, a->softmax_scale, sl2, lse2, delta, sq_pad, hsplit, dkv_part, stamps, kg));
   }
   if (hsplit > 1) {
     const int kv_blocks = pico_cdiv(a->batch * a->seqlen_k * a->heads_kv * (D / 16), 256);

@@ -23,9 +23,12 @@ CASES = {  # B, S, Hq, Hkv, D, causal
     "full": (2, 1024, 8, 8, 64, False),
     "fold5": (6, 640, 32, 32, 64, True),      # 5 blocks x 192 heads > one round: one folded pair per head
     "fold_ragged": (7, 1000, 32, 32, 64, True),  # ragged last block inside a folded pair
-    "d128": (2, 1024, 16, 16, 128, True),   # Llama-2-7B per tp-2 rank
+    "grp_ragged": (4, 1000, 32, 32, 64, True),   # one-round block groups (dQ and dK/dV) with a ragged last block
+    "grp_10": (4, 1280, 32, 32, 64, True),       # ten blocks per head into six groups
+    "d128": (4, 1024, 16, 16, 128, True),   # Llama-2-7B per tp-2 rank, the reference's micro-batch 4
+    "d128_b2": (2, 1024, 16, 16, 128, True),
     "d128_ragged": (1, 1000, 8, 8, 128, True),
-    "d128_full": (2, 1024, 16, 16, 128, False),
+    "d128_full": (4, 1024, 16, 16, 128, False),
     "d128_s4096": (1, 4096, 16, 16, 128, True),
 }
 

@@ -1,7 +1,7 @@
 """Which parameters' gradients reach an AccumulateGrad node through autograd in the pipelined micro-batch graph
 (torch's "AccumulateGrad node's stream does not match ..." warning in
 test_wgrad_pairs_match_unpaired[4-False-True]). The test's model and step (4 micro-batches, no DP, pipelined graph):
-every parameter gets a tensor hook (called with a DEFINED incoming gradient only) that records the parameter, the
+every parameter gets a tensor hook (called with the incoming gradient; None ones are skipped) that records the parameter, the
 micro-batch announced to wgrad_pair and the current stream; warnings are recorded per step."""
 import os
 import sys
@@ -30,7 +30,8 @@ def main():
     seen = []
     for name, p in m.named_parameters():
         def hook(g, name=name):
-            seen.append((name, WP._CTX["i"], torch.cuda.current_stream().stream_id, tuple(g.shape)))
+            if g is not None:
+                seen.append((name, WP._CTX["i"], torch.cuda.current_stream().stream_id, tuple(g.shape)))
             return g
         p.register_hook(hook)
 
