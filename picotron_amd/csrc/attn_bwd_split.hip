@@ -148,7 +148,7 @@ template <int D, bool CAUSAL>
 __global__ __launch_bounds__(256, QCfg<D>::MINB) void attn_bwd_q_kernel(const pico_attn_args a, float scale, float scale_log2,
                                                              float* __restrict__ lse2_g, float* __restrict__ delta_g,
                                                              int sq_pad, unsigned long long* __restrict__ stamp_out,
-                                                             int nfront) {
+                                                             int nfront, float lse_mul, float lse_pad) {
   using C = QCfg<D>;
 #if PICO_BWDQ_WGSTAMP
   unsigned long long wgs[4];
@@ -257,8 +257,9 @@ __global__ __launch_bounds__(256, QCfg<D>::MINB) void attn_bwd_q_kernel(const pi
   const bool row_ok = my_q < Sq;
   const float delta = row_ok ? dall : 0.f;
   const float lse2 = row_ok ? a.lse[((int64_t)b * a.heads_q + hq) * Sq + my_q] * LOG2E : INFINITY;
-  if (h == 0 && my_q < sq_pad) {  // for attn_bwd_kv_kernel (padding rows: P = 0, delta = 0)
-    lse2_g[(int64_t)bh * sq_pad + my_q] = lse2;
+  if (h == 0 && my_q < sq_pad) {  // for the dK/dV kernel (padding rows: P = 0, delta = 0)
+    // attn_bwd_kv_kernel: LSE log2 e (+inf padding); attn_bwd_kvp_kernel: -LSE / scale (-inf padding)
+    lse2_g[(int64_t)bh * sq_pad + my_q] = row_ok ? a.lse[((int64_t)b * a.heads_q + hq) * Sq + my_q] * lse_mul : lse_pad;
     delta_g[(int64_t)bh * sq_pad + my_q] = -delta;
   }
 
@@ -828,7 +829,436 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kv_kernel(const pico_
 #endif
 }
 
-int split_sq_pad(const pico_attn_args* a) { return (int)((a->seqlen_q + QT - 1) / QT) * QT; }
+#ifndef PICO_SPLIT_D128_TU
+// ------------------------------------------------------------------------------------------------
+// dK / dV kernel, D = 64, 64-row query tiles in a hand-ordered stream (round 5; PICO_ATTN_KVP)
+// ------------------------------------------------------------------------------------------------
+// The same work as attn_bwd_kv_kernel (key on the lane, 32 keys per wave, 128 keys per workgroup, K / V fragments
+// resident), but each ring tile is 64 query rows, two 32-row halves A and B whose phases interleave inside one
+// wave: M1 = S and dP (8 MFMAs per half), V = the softmax VALU (P = exp2(c S'), dS = P dP, packed to bf16), M2 =
+// dV^T += dO^T P and dK^T += Q^T dS (8 MFMAs per half). The 32-row kernel's tile is one dependency chain
+// (M1 -> V -> M2, every operand read right before its MFMA: 19 waits per tile, ~1 us per tile for a wave
+// alone); here a tile is the stream
+//     M1(A) | reads of B's operands,  M1(B) | V(A) + A's transposed reads,  M2(A) | V(B) + B's reads,  M2(B)
+// so every MFMA gap carries independent work (the guide's per-gap budget: <= 5 fillers, one transcendental),
+// one barrier and one DMA round serve 64 rows, and two waves per SIMD (two workgroups per CU, <= 256 VGPRs)
+// fill each other's remaining gaps. Row constants enter as the initial accumulators (no subtraction, no LSE
+// registers): S' = Q K^T - LSE / scale (the dQ kernel writes -LSE / scale for these rows, -inf for padding
+// rows; the causal / padding-key mask sets -inf in that initial value on diagonal tiles) and dP' = dO V^T - delta.
+constexpr int QT2 = 64;
+struct KVPCfg {
+  static constexpr int D = 64, KS = 4, DT = 2, CPR = 8, RB = 128;
+  static constexpr int QIMG = QT2 * RB;          // one Q (or dO) 64-row image, 8 KiB
+  static constexpr int LSD = 1024;               // -LSE/scale [64] | -delta [64] (+ 512 B the DMA piece repeats)
+  static constexpr int SLOT = 2 * QIMG + LSD;    // 17 KiB; 3 slots = 51 KiB per workgroup
+  static constexpr int NBUF = 3, PD = 2;
+  static constexpr int RPP = 1024 / RB;          // 8 image rows per 1-KiB piece
+  static constexpr int NQP = QIMG / 1024;        // 8 pieces per image
+  static constexpr int NP = 2 * NQP + 1;         // 17 pieces per tile: 4 per wave + wave 0's LSE / delta piece
+};
+
+#define KVP_SLOT() __builtin_amdgcn_sched_barrier(0)
+
+template <bool CAUSAL, int MINB>
+__global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kvp_kernel(const pico_attn_args a, float scale, float c2,
+                                                                const float* __restrict__ sinit_g,
+                                                                const float* __restrict__ delta_g, int sq_pad,
+                                                                int hsplit, float* __restrict__ dkv_part,
+                                                                const BlkGroups grp) {
+  using C = KVPCfg;
+  constexpr int KS = C::KS, DT = C::DT, CPR = C::CPR, RB = C::RB;
+  static_assert(C::NP == 4 * KNW + 1, "four Q / dO pieces per wave + one LSE / delta piece");
+  __shared__ __attribute__((aligned(16))) char smem[C::NBUF * C::SLOT];
+
+  const int lane0 = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int Sq = (int)a.seqlen_q, Sk = (int)a.seqlen_k;
+  const int Hq = (int)a.heads_q;
+  const int G = (int)(a.heads_q / a.heads_kv);
+  const int nbh = (int)(a.batch * a.heads_kv) * hsplit;
+  const int gi = blockIdx.x / nbh;
+  const int bhs = blockIdx.x % nbh;
+  const int hs = bhs % hsplit;
+  const int bh = bhs / hsplit;
+  const int b = bh / (int)a.heads_kv, hk = bh % (int)a.heads_kv;
+  const unsigned gw = grp.n ? grp_sel(grp, gi) : 0u;
+  const int nblk_wg = grp.n ? (int)((grp.cnt >> (4 * gi)) & 15u) : 1;
+  const unsigned delta_off = (unsigned)((const char*)delta_g - (const char*)sinit_g);  // same workspace
+  const unsigned ring_lds = (unsigned)__builtin_amdgcn_readfirstlane((int)lds_addr(smem));
+#pragma clang loop unroll(disable)
+  for (int jb = 0; jb < nblk_wg; ++jb) {
+  const int kb = grp.n ? (int)((gw >> (8 * jb)) & 255u) : gi;
+  if (jb > 0) lds_barrier();
+  int lane_l = lane0;
+  asm volatile("" : "+v"(lane_l));
+  const int lane = lane_l, r = lane & 31, h = lane >> 5;
+  const int k0 = kb * KVB;
+  const int kw = k0 + 32 * wave;
+  const int qstart = CAUSAL ? k0 : 0;  // k0 is a multiple of QT2
+  const int nqt = Sq > qstart ? (Sq - qstart + QT2 - 1) / QT2 : 0;
+  const int ntot = G * nqt;
+  const int tb = (int)((int64_t)ntot * hs / hsplit);
+  const int ntiles = (int)((int64_t)ntot * (hs + 1) / hsplit) - tb;
+  const int hq0 = hk * G + (nqt ? tb / nqt : 0), q00 = qstart + (nqt ? tb % nqt : 0) * QT2;
+
+  // ---- tile DMA: this wave's pieces i = 0..3 are image pieces j = wave + 4 i (Q: j < 8, dO: 8 <= j < 16);
+  // wave 0 also issues the LSE / delta piece (lanes 0-15: -LSE/scale rows 4l..4l+3, 16-31: -delta rows, 32-63
+  // repeat 0-31)
+  const int64_t qs1 = a.q_strides[1] * 2, ds1 = a.do_strides[1] * 2;  // bytes per query row
+  const char* const qbase = (const char*)((const bf16_t*)a.q + b * a.q_strides[0]);
+  const char* const dobase = (const char*)((const bf16_t*)a.dout + b * a.do_strides[0]);
+  int pc_row[4];
+  unsigned pc_off[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int jj = (wave + 4 * i) % C::NQP;
+    pc_row[i] = C::RPP * jj + lane / CPR;
+    pc_off[i] = (unsigned)(pc_row[i] * (i < 2 ? qs1 : ds1) + 8 * ((lane % CPR) ^ swz<64>(pc_row[i])) * 2);
+  }
+  struct Tc {
+    int hq, q0;
+    const char* qp;
+    const char* dp;
+    const char* lp;
+  };
+  auto make_tc = [&](int hq, int q0) __attribute__((always_inline)) {
+    Tc c;
+    c.hq = hq;
+    c.q0 = q0;
+    c.qp = qbase + hq * a.q_strides[2] * 2 + q0 * qs1;
+    c.dp = dobase + hq * a.do_strides[2] * 2 + q0 * ds1;
+    c.lp = (const char*)(sinit_g + ((int64_t)b * Hq + hq) * sq_pad + q0);
+    return c;
+  };
+  const int qend = qstart + nqt * QT2;
+  auto advance = [&](Tc& c) __attribute__((always_inline)) {
+    if (c.q0 + QT2 >= qend) {
+      c = make_tc(c.hq + 1, qstart);
+    } else {
+      c.q0 += QT2;
+      c.qp += QT2 * qs1;
+      c.dp += QT2 * ds1;
+      c.lp += QT2 * 4;
+    }
+  };
+  const bool ragged = Sq % QT2 != 0;
+  auto issue = [&](int si, const Tc& c) __attribute__((always_inline)) {
+    const unsigned dst = ring_lds + (unsigned)si * (unsigned)C::SLOT;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int jj = (wave + 4 * i) % C::NQP;
+      unsigned off = pc_off[i];
+      if (ragged && c.q0 + QT2 > Sq) {  // partial tile: rows past Sq - 1 clamped (finite; their LSE is +inf)
+        int l2 = lane0;
+        asm volatile("" : "+v"(l2));
+        const int row = C::RPP * jj + (l2 & 63) / CPR;
+        off = (unsigned)((min(c.q0 + row, Sq - 1) - c.q0) * (i < 2 ? qs1 : ds1) +
+                         8 * (((l2 & 63) % CPR) ^ swz<64>(row)) * 2);
+      }
+      dma_piece(i < 2 ? c.qp : c.dp, off, dst + (i < 2 ? 0u : (unsigned)C::QIMG) + (unsigned)jj * 1024u);
+    }
+    if (wave == 0) {
+      int l = lane0;
+      asm volatile("" : "+v"(l));
+      l &= 31;
+      dma_piece(c.lp, (unsigned)(16 * (l & 15)) + ((l >> 4) ? delta_off : 0u), dst + 2u * C::QIMG);
+    }
+  };
+  Tc nxt = make_tc(hq0, q00);
+#pragma unroll
+  for (int j = 0; j < C::PD; ++j) {
+    if (j < ntiles) issue(j, nxt);
+    advance(nxt);
+  }
+
+  // ---- K, V fragments of this wave's 32 keys (B operands of S and dP) ----
+  const bf16_t* kg = (const bf16_t*)a.k + b * a.k_strides[0] + hk * a.k_strides[2];
+  const bf16_t* vg = (const bf16_t*)a.v + b * a.v_strides[0] + hk * a.v_strides[2];
+  bf16x8 kf[KS], vf[KS];
+  {
+    const int key = kw + r;
+    const bool ok = key < Sk;
+    const bf16_t* kp = kg + (int64_t)min(key, Sk - 1) * a.k_strides[1] + 8 * h;
+    const bf16_t* vp = vg + (int64_t)min(key, Sk - 1) * a.v_strides[1] + 8 * h;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const u16x8 kv = *reinterpret_cast<const u16x8*>(kp + 16 * ks);
+      const u16x8 vv = *reinterpret_cast<const u16x8*>(vp + 16 * ks);
+      kf[ks] = __builtin_bit_cast(bf16x8, ok ? kv : (u16x8)0);
+      vf[ks] = __builtin_bit_cast(bf16x8, ok ? vv : (u16x8)0);
+    }
+  }
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) asm volatile("" : "+v"(kf[ks]), "+v"(vf[ks]));
+  f32x16 dk[DT], dv[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) {
+    dk[dt] = (f32x16)0.f;
+    dv[dt] = (f32x16)0.f;
+  }
+  unsigned qo[KS], tro[DT][2];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) qo[ks] = lds_off<64>(r, 2 * ks + h);
+  tr_offsets<64>(lane, tro);
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) asm volatile("" : "+v"(qo[ks]));
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) asm volatile("" : "+v"(tro[dt][0]), "+v"(tro[dt][1]));
+  const bool kpad = kw + 31 >= Sk;  // wave-uniform: some of the wave's keys are padding
+  const int mykey = kw + r;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // the initial accumulator of half X (rows 32 X + 8 g + 4 h + j of the lane's registers 4 g + j) from the
+  // tile's LSE / delta piece: which = 0 -> -LSE/scale, 1 -> -delta
+  auto init_rows = [&](const float* lsd, int X, int which) __attribute__((always_inline)) {
+    f32x16 v;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 t4 = *reinterpret_cast<const f32x4*>(lsd + 64 * which + 32 * X + 8 * g + 4 * h);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[4 * g + j] = t4[j];
+    }
+    return v;
+  };
+  // diagonal / padding-key mask on an S initial value: -inf where key > query row (causal) or key >= Sk
+  auto mask_rows = [&](f32x16& s, int qrow0) __attribute__((always_inline)) {
+    const int rel = mykey >= Sk ? 1 << 30 : (CAUSAL ? mykey - qrow0 - 4 * h : -1);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s[i] = ((i & 3) + 8 * (i >> 2) < rel) ? -INFINITY : s[i];
+  };
+  int q0cur = q00;
+  for (int t0 = 0; t0 < ntiles; t0 += C::NBUF) {
+#pragma unroll
+    for (int u = 0; u < C::NBUF; ++u) {
+      const int t = t0 + u;
+      if (t >= ntiles) break;
+      if (t > 0) {
+        if (t + 2 <= ntiles) {  // tile t + 1 stays in flight
+          if (wave == 0) wait_vmcnt(5);
+          else wait_vmcnt(4);
+        } else {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        lds_barrier();  // every wave's pieces of tile t visible; the slot of tile t - 1 is no longer read
+      }
+      if (t + C::PD < ntiles) issue((u + C::PD) % C::NBUF, nxt);
+      advance(nxt);
+      KVP_SLOT();
+      const char* qs = smem + u * C::SLOT;
+      const char* dos = qs + C::QIMG;
+      const float* lsd = (const float*)(qs + 2 * C::QIMG);
+      const bool diag = (CAUSAL && kw + 31 > q0cur) || kpad;        // half A has masked elements
+      const bool diagB = (CAUSAL && kw + 31 > q0cur + 32) || kpad;  // half B has masked elements
+
+      // The tile as 32 MFMA slots (one MFMA each, KVP_SLOT fences between them; every wait the compiler adds is a
+      // counted lgkmcnt on reads issued two or more slots earlier):
+      //   a1-a8 M1(A)  | Q / dO fragments of A and B, B's initial values
+      //   b1-b8 M1(B)  | V(A) (one element pair per slot: 2 mul, 2 exp, 2 mul, 2 cvt_pk), A's transposed operands
+      //   c1-c8 M2(A)  | V(A) tail, V(B), B's transposed operands
+      //   d1-d8 M2(B)  | V(B) tail
+      bf16x8 qa[KS], da[KS], qb[KS], db[KS];
+      bf16x8 toA[2][DT], tqA[2][DT], toB[2][DT], tqB[2][DT];
+      unsigned pwA[8], swA[8], pwB[8], swB[8];  // packed P / dS pairs: element pair e of a half -> word e
+      auto vpair = [&](const f32x16& sv, const f32x16& dpv, int e, unsigned& pw, unsigned& sw)
+          __attribute__((always_inline)) {
+        typedef __attribute__((ext_vector_type(2))) float f32x2;
+        typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+        const float p0 = fast_exp2(sv[2 * e] * c2), p1 = fast_exp2(sv[2 * e + 1] * c2);
+        pw = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){p0, p1}, bf16x2));
+        sw = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){p0 * dpv[2 * e], p1 * dpv[2 * e + 1]}, bf16x2));
+      };
+      auto pk4 = [&](const unsigned* w) __attribute__((always_inline)) {
+        typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+        return __builtin_bit_cast(bf16x8, (u32x4){w[0], w[1], w[2], w[3]});
+      };
+      // A's operands and initial values (their latency is the one exposed read of the tile)
+      qa[0] = lds_read_b128(qs, qo[0]);
+      qa[1] = lds_read_b128(qs, qo[1]);
+      f32x16 sA = init_rows(lsd, 0, 0);
+      f32x16 dpA = init_rows(lsd, 0, 1);
+      if (diag) mask_rows(sA, q0cur);
+      f32x16 sB, dpB;
+      KVP_SLOT();
+      sA = mfma32(qa[0], kf[0], sA);  // a1
+      qa[2] = lds_read_b128(qs, qo[2]);
+      qa[3] = lds_read_b128(qs, qo[3]);
+      KVP_SLOT();
+      sA = mfma32(qa[1], kf[1], sA);  // a2
+      da[0] = lds_read_b128(dos, qo[0]);
+      da[1] = lds_read_b128(dos, qo[1]);
+      KVP_SLOT();
+      sA = mfma32(qa[2], kf[2], sA);  // a3
+      da[2] = lds_read_b128(dos, qo[2]);
+      da[3] = lds_read_b128(dos, qo[3]);
+      KVP_SLOT();
+      sA = mfma32(qa[3], kf[3], sA);  // a4
+      sB = init_rows(lsd, 1, 0);
+      KVP_SLOT();
+      dpA = mfma32(da[0], vf[0], dpA);  // a5
+      dpB = init_rows(lsd, 1, 1);
+      KVP_SLOT();
+      dpA = mfma32(da[1], vf[1], dpA);  // a6
+      qb[0] = lds_read_b128(qs, qo[0] + 32 * RB);
+      qb[1] = lds_read_b128(qs, qo[1] + 32 * RB);
+      if (diagB) mask_rows(sB, q0cur + 32);
+      KVP_SLOT();
+      dpA = mfma32(da[2], vf[2], dpA);  // a7
+      qb[2] = lds_read_b128(qs, qo[2] + 32 * RB);
+      qb[3] = lds_read_b128(qs, qo[3] + 32 * RB);
+      KVP_SLOT();
+      dpA = mfma32(da[3], vf[3], dpA);  // a8
+      db[0] = lds_read_b128(dos, qo[0] + 32 * RB);
+      db[1] = lds_read_b128(dos, qo[1] + 32 * RB);
+      KVP_SLOT();
+      sB = mfma32(qb[0], kf[0], sB);  // b1
+      db[2] = lds_read_b128(dos, qo[2] + 32 * RB);
+      db[3] = lds_read_b128(dos, qo[3] + 32 * RB);
+      KVP_SLOT();
+      sB = mfma32(qb[1], kf[1], sB);  // b2
+      toA[0][0] = tr_pair(dos, tro[0][0], tro[0][1]);
+      KVP_SLOT();
+      sB = mfma32(qb[2], kf[2], sB);  // b3
+      vpair(sA, dpA, 0, pwA[0], swA[0]);
+      tqA[0][0] = tr_pair(qs, tro[0][0], tro[0][1]);
+      KVP_SLOT();
+      sB = mfma32(qb[3], kf[3], sB);  // b4
+      vpair(sA, dpA, 1, pwA[1], swA[1]);
+      toA[0][1] = tr_pair(dos, tro[1][0], tro[1][1]);
+      KVP_SLOT();
+      dpB = mfma32(db[0], vf[0], dpB);  // b5
+      vpair(sA, dpA, 2, pwA[2], swA[2]);
+      tqA[0][1] = tr_pair(qs, tro[1][0], tro[1][1]);
+      KVP_SLOT();
+      dpB = mfma32(db[1], vf[1], dpB);  // b6
+      vpair(sA, dpA, 3, pwA[3], swA[3]);
+      toA[1][0] = tr_pair(dos + 16 * RB, tro[0][0], tro[0][1]);
+      KVP_SLOT();
+      dpB = mfma32(db[2], vf[2], dpB);  // b7
+      vpair(sA, dpA, 4, pwA[4], swA[4]);
+      tqA[1][0] = tr_pair(qs + 16 * RB, tro[0][0], tro[0][1]);
+      KVP_SLOT();
+      dpB = mfma32(db[3], vf[3], dpB);  // b8
+      vpair(sA, dpA, 5, pwA[5], swA[5]);
+      toA[1][1] = tr_pair(dos + 16 * RB, tro[1][0], tro[1][1]);
+      KVP_SLOT();
+      const bf16x8 pA0 = pk4(pwA), sA0 = pk4(swA);
+      dv[0] = mfma32(toA[0][0], pA0, dv[0]);  // c1
+      vpair(sA, dpA, 6, pwA[6], swA[6]);
+      tqA[1][1] = tr_pair(qs + 16 * RB, tro[1][0], tro[1][1]);
+      KVP_SLOT();
+      dk[0] = mfma32(tqA[0][0], sA0, dk[0]);  // c2
+      vpair(sA, dpA, 7, pwA[7], swA[7]);
+      toB[0][0] = tr_pair(dos + 32 * RB, tro[0][0], tro[0][1]);
+      KVP_SLOT();
+      dv[1] = mfma32(toA[0][1], pA0, dv[1]);  // c3
+      vpair(sB, dpB, 0, pwB[0], swB[0]);
+      tqB[0][0] = tr_pair(qs + 32 * RB, tro[0][0], tro[0][1]);
+      KVP_SLOT();
+      dk[1] = mfma32(tqA[0][1], sA0, dk[1]);  // c4
+      vpair(sB, dpB, 1, pwB[1], swB[1]);
+      toB[0][1] = tr_pair(dos + 32 * RB, tro[1][0], tro[1][1]);
+      KVP_SLOT();
+      const bf16x8 pA1 = pk4(pwA + 4), sA1 = pk4(swA + 4);
+      dv[0] = mfma32(toA[1][0], pA1, dv[0]);  // c5
+      vpair(sB, dpB, 2, pwB[2], swB[2]);
+      tqB[0][1] = tr_pair(qs + 32 * RB, tro[1][0], tro[1][1]);
+      KVP_SLOT();
+      dk[0] = mfma32(tqA[1][0], sA1, dk[0]);  // c6
+      vpair(sB, dpB, 3, pwB[3], swB[3]);
+      toB[1][0] = tr_pair(dos + 48 * RB, tro[0][0], tro[0][1]);
+      KVP_SLOT();
+      dv[1] = mfma32(toA[1][1], pA1, dv[1]);  // c7
+      vpair(sB, dpB, 4, pwB[4], swB[4]);
+      tqB[1][0] = tr_pair(qs + 48 * RB, tro[0][0], tro[0][1]);
+      KVP_SLOT();
+      dk[1] = mfma32(tqA[1][1], sA1, dk[1]);  // c8
+      vpair(sB, dpB, 5, pwB[5], swB[5]);
+      toB[1][1] = tr_pair(dos + 48 * RB, tro[1][0], tro[1][1]);
+      KVP_SLOT();
+      const bf16x8 pB0 = pk4(pwB), sB0 = pk4(swB);
+      dv[0] = mfma32(toB[0][0], pB0, dv[0]);  // d1
+      vpair(sB, dpB, 6, pwB[6], swB[6]);
+      tqB[1][1] = tr_pair(qs + 48 * RB, tro[1][0], tro[1][1]);
+      KVP_SLOT();
+      dk[0] = mfma32(tqB[0][0], sB0, dk[0]);  // d2
+      vpair(sB, dpB, 7, pwB[7], swB[7]);
+      KVP_SLOT();
+      dv[1] = mfma32(toB[0][1], pB0, dv[1]);  // d3
+      KVP_SLOT();
+      dk[1] = mfma32(tqB[0][1], sB0, dk[1]);  // d4
+      KVP_SLOT();
+      const bf16x8 pB1 = pk4(pwB + 4), sB1 = pk4(swB + 4);
+      dv[0] = mfma32(toB[1][0], pB1, dv[0]);  // d5
+      KVP_SLOT();
+      dk[0] = mfma32(tqB[1][0], sB1, dk[0]);  // d6
+      KVP_SLOT();
+      dv[1] = mfma32(toB[1][1], pB1, dv[1]);  // d7
+      KVP_SLOT();
+      dk[1] = mfma32(tqB[1][1], sB1, dk[1]);  // d8
+      KVP_SLOT();
+      q0cur = q0cur + QT2 >= qend ? qstart : q0cur + QT2;
+    }
+  }
+
+  // ---- epilogue (as attn_bwd_kv_kernel): lane = key kw + r, register i of tile dt = d 32 dt + acc_row(i, h) ----
+  if (hsplit == 1) {
+    const int key = kw + r;
+    const int kc = min(key, Sk - 1);
+    if (a.flags & PICO_ATTN_ROPE_BWD) {
+      const bf16_t* cp = (const bf16_t*)a.rope_cos + (int64_t)kc * a.rope_stride;
+      const bf16_t* sp = (const bf16_t*)a.rope_sin + (int64_t)kc * a.rope_stride;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const u16x4 c4 = *reinterpret_cast<const u16x4*>(cp + 8 * g + 4 * h);
+        const u16x4 s4 = *reinterpret_cast<const u16x4*>(sp + 8 * g + 4 * h);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float cf = bf2f(c4[j]), sn = bf2f(s4[j]);
+          const float x1 = dk[0][4 * g + j], x2 = dk[1][4 * g + j];
+          dk[0][4 * g + j] = x1 * cf + x2 * sn;
+          dk[1][4 * g + j] = x2 * cf - x1 * sn;
+        }
+      }
+    }
+    bf16_t* dkp = (bf16_t*)a.dk + b * a.dk_strides[0] + hk * a.dk_strides[2] + (int64_t)kc * a.dk_strides[1];
+    bf16_t* dvp = (bf16_t*)a.dv + b * a.dv_strides[0] + hk * a.dv_strides[2] + (int64_t)kc * a.dv_strides[1];
+    store_row_bf16_x16<DT>(dkp, h, key < Sk, [&](int dt, int i) { return dk[dt][i] * scale; });
+    store_row_bf16_x16<DT>(dvp, h, key < Sk, [&](int dt, int i) { return dv[dt][i]; });
+  } else {  // fp32 partials [hs][dK | dV][b][key][hk][D]
+    const int64_t part = a.batch * a.seqlen_k * a.heads_kv * 64;
+    float* pk = dkv_part + (int64_t)(2 * hs) * part + ((int64_t)b * Sk * a.heads_kv + hk) * 64;
+    float* pv = pk + part;
+    const int key = kw + r;
+    if (key < Sk) {
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          f32x4 wk, wv;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            wk[j] = dk[dt][4 * g + j] * scale;
+            wv[j] = dv[dt][4 * g + j];
+          }
+          const int64_t o = (int64_t)key * a.heads_kv * 64 + 32 * dt + 8 * g + 4 * h;
+          *reinterpret_cast<f32x4*>(pk + o) = wk;
+          *reinterpret_cast<f32x4*>(pv + o) = wv;
+        }
+    }
+  }
+  }  // key blocks of the group
+}
+#undef KVP_SLOT
+
+bool kvp_enabled() {
+  const char* e = getenv("PICO_ATTN_KVP");
+  return e && e[0] == '1';
+}
+#endif  // !PICO_SPLIT_D128_TU
+
+// rows of the LSE / delta workspace per (batch, head): padded to the 64-row tiles of attn_bwd_kvp_kernel
+int split_sq_pad(const pico_attn_args* a) { return (int)((a->seqlen_q + 63) / 64) * 64; }
 
 int64_t split_lsd_floats(const pico_attn_args* a) {
   const int64_t n = a->batch * a->heads_q * (int64_t)split_sq_pad(a);
@@ -842,6 +1272,9 @@ int64_t split_lsd_floats(const pico_attn_args* a) {
 // registers: its own translation unit, AGPRs allowed).
 int kv_minb(const pico_attn_args* a) {
   if (a->head_dim == 128) return 1;
+#ifndef PICO_SPLIT_D128_TU
+  if (kvp_enabled()) return 2;  // attn_bwd_kvp_kernel: two waves per SIMD, <= 256 VGPRs
+#endif
   return a->causal ? 3 : 2;
 }
 
@@ -941,19 +1374,30 @@ int launch_split(const pico_attn_args* a, hipStream_t s) {
   float* delta = lse2 + split_lsd_floats(a);
   float* dkv_part = delta + split_lsd_floats(a);
   const float sl2 = a->softmax_scale * LOG2E;
+#ifndef PICO_SPLIT_D128_TU
+  const bool use_kvp = D == 64 && kvp_enabled();
+#else
+  constexpr bool use_kvp = false;
+#endif
   const int nmb = (int)((a->seqlen_q + QB - 1) / QB);
   const int64_t gq = (int64_t)nmb * a->batch * a->heads_q;
   PICO_REQUIRE(gq < (1ll << 31), "pico_attn_bwd: grid too large");
   PICO_TRY(pico_launch(PICO_K_ATTN_BWD_Q, "attn_bwd_q", attn_bwd_q_kernel<D, CAUSAL>, dim3((int)gq), dim3(256), 0, s,
                        *a, a->softmax_scale, sl2, lse2, delta, sq_pad,
                        (unsigned long long*)((char*)a->workspace + pico_attn_bwd_split_workspace(a) - STAMP_BYTES),
-                       q_front(a)));
+                       q_front(a), use_kvp ? -1.0f / a->softmax_scale : LOG2E, use_kvp ? -INFINITY : INFINITY));
   const int nkb = (int)((a->seqlen_k + KVB - 1) / KVB);
   const int hsplit = kv_hsplit(a);
   const BlkGroups kg = kv_groups(a, hsplit, kv_minb(a));
   const int64_t nblk = (int64_t)(kg.n ? kg.n : nkb) * a->batch * a->heads_kv * hsplit;
   if (nblk == 0) return 0;
   unsigned long long* stamps = (unsigned long long*)((char*)a->workspace + pico_attn_bwd_split_workspace(a) - STAMP_BYTES);
+#ifndef PICO_SPLIT_D128_TU
+  if (use_kvp) {
+    PICO_TRY(pico_launch(PICO_K_ATTN_BWD_KV, "attn_bwd_kv", attn_bwd_kvp_kernel<CAUSAL, 2>, dim3((int)nblk),
+                         dim3(KNW * 64), 0, s, *a, a->softmax_scale, sl2, lse2, delta, sq_pad, hsplit, dkv_part, kg));
+  } else
+#endif
   if constexpr (D == 128) {
     PICO_TRY(pico_launch(PICO_K_ATTN_BWD_KV, "attn_bwd_kv", attn_bwd_kv_kernel<D, CAUSAL, 1>, dim3((int)nblk),
                          dim3(KNW * 64), 0, s, *a, a->softmax_scale, sl2, lse2, delta, sq_pad, hsplit, dkv_part, stamps, kg));

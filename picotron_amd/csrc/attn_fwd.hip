@@ -7,8 +7,8 @@
 //
 // Structure (one workgroup = 4 waves = 128 query rows of one (batch, q-head); 64-key tiles):
 //   * Q stays in registers for the whole sweep (B operand, 8 bf16 per lane per 16-wide k-step).
-//   * K and V tiles are register-staged into a double-buffered, XOR-swizzled LDS image: the next
-//     tile's global loads are issued before this tile's MFMAs and written to LDS after them (T14).
+//   * K and V tiles arrive by LDS-DMA (global_load_lds_dwordx4, the swizzle applied to the per-lane source
+//     address) into an NBUF-slot ring of conflict-free LDS images, prefetch distance NBUF - 1 (below).
 //   * Swapped product S^T = K * Q^T (v_mfma_f32_32x32x16_bf16): the accumulator has the query on
 //     the lane and 16 keys in registers, so the online softmax is lane-local (one permlane32 swap
 //     for the row max) and P^T is already the B operand of O^T += V^T * P^T (no LDS round trip);
@@ -74,12 +74,6 @@ namespace {
 constexpr int BM = 128;  // query rows per workgroup (32 per wave)
 constexpr int BN = 64;   // keys per tile
 
-// LDS images (one per buffer), chosen so that every read of a tile is one per-lane base register
-// plus compile-time immediates, and conflict-free:
-//   K: KS images [64 keys][16 d] (32-B rows), 16-B chunk h of row `key` stored at chunk h ^ bit3(key):
-//      a ds_read_b128 lane group (16 rows, one chunk) covers all 64 banks exactly once;
-//   V: D/32 images [64 keys][32 d] (64-B rows), unswizzled: each 32-lane half of a ds_read_b64_tr_b16
-//      reads 4 consecutive rows x 64 B = 256 contiguous bytes.
 // LDS images (one set per ring slot), chosen so that every read of a tile is one per-lane base
 // register plus compile-time immediates, and conflict-free:
 //   K: KS images [64 keys][16 d] (32-B rows), 16-B chunk h of row `key` stored at chunk h ^ bit3(key):
