@@ -56,7 +56,13 @@ constexpr int QT = 32;                    // dkv kernel: query rows per tile
 #ifndef PICO_BWDQ_WGSTAMP
 #define PICO_BWDQ_WGSTAMP 0
 #endif
-constexpr int64_t STAMP_BYTES = (PICO_BWDKV_WGSTAMP || PICO_BWDQ_WGSTAMP) ? 65536 * 4 * 8 : 0;
+// PICO_KVP_STAMP: diagnostic build — every wave of attn_bwd_kvp_kernel accumulates s_memtime (shader clock)
+// deltas per phase of its tiles (wait, barrier, DMA issue, M1(A), M1(B), M2(A), M2(B)) and the tile count:
+// 8 x 8 B per wave at stamp_out[(block * 4 + wave) * 8] (scripts/kvp_stamps.py)
+#ifndef PICO_KVP_STAMP
+#define PICO_KVP_STAMP 0
+#endif
+constexpr int64_t STAMP_BYTES = (PICO_BWDKV_WGSTAMP || PICO_BWDQ_WGSTAMP || PICO_KVP_STAMP) ? 65536 * 4 * 8 : 0;
 
 // dQ kernel: ring slots and workgroups per CU the register budget is sized for. D = 64: 3 slots (48 KiB), three
 // workgroups per CU at 168 VGPRs (the two 32-key halves of a tile in turn: C2 45.7 -> 44.1 us, S 4096 115.9 ->
@@ -68,7 +74,10 @@ struct QCfg {
   static constexpr int MINB = D == 64 ? 3 : 2;   // workgroups per CU (register budget 168 / 248 VGPRs)
   static constexpr int IMG = KT * RB;            // one K (or V) tile image (lds_off<D> layout)
   static constexpr int SLOT = 2 * IMG;           // K | V
-  static constexpr int NBUF = D == 64 ? 3 : 2;   // ring slots; prefetch NBUF - 1
+#ifndef PICO_Q_NBUF64
+#define PICO_Q_NBUF64 3
+#endif
+  static constexpr int NBUF = D == 64 ? PICO_Q_NBUF64 : 2;   // ring slots; prefetch NBUF - 1
   static constexpr int RPP = 1024 / RB;        // image rows per 1-KiB DMA piece
   static constexpr int NP = SLOT / 1024;       // pieces per tile
   static constexpr int NPW = NP / 4;           // per wave
@@ -80,8 +89,11 @@ struct KVCfg {
   static constexpr int QIMG = QT * RB;   // one Q (or dO) tile image
   static constexpr int LSD = 1024;       // LSE*log2e [32] | -delta [32] (one DMA piece)
   static constexpr int SLOT = 2 * QIMG + LSD;
-  static constexpr int PD = 2;    // prefetch distance (tiles)
-  static constexpr int NBUF = 3;  // ring slots
+#ifndef PICO_KV_NBUF
+#define PICO_KV_NBUF 3
+#endif
+  static constexpr int NBUF = PICO_KV_NBUF;  // ring slots
+  static constexpr int PD = NBUF - 1;        // prefetch distance (tiles)
   static constexpr int RPP = 1024 / RB;
   static constexpr int NQP = QIMG / 1024;
   static constexpr int NP = 2 * NQP + 1;
@@ -144,8 +156,11 @@ PICO_DEV void tr_offsets(int lane, unsigned (&tro)[D / 32][2]) {
 // ------------------------------------------------------------------------------------------------
 // dQ kernel (query-major)
 // ------------------------------------------------------------------------------------------------
-template <int D, bool CAUSAL>
-__global__ __launch_bounds__(256, QCfg<D>::MINB) void attn_bwd_q_kernel(const pico_attn_args a, float scale, float scale_log2,
+// PIPE (D = 64, opt-in PICO_ATTN_QP=1, round 5): the tile's two 32-key halves as one hand-ordered stream of 24
+// MFMA slots instead of one after the other — M1(h0) | h1's K / V fragments, M1(h1) | V(h0) and h0's transposed
+// K operands, M2(h0) | V(h1), M2(h1) — at two workgroups per CU (<= 256 VGPRs; as attn_bwd_kvp_kernel).
+template <int D, bool CAUSAL, bool PIPE = false>
+__global__ __launch_bounds__(256, PIPE ? 2 : QCfg<D>::MINB) void attn_bwd_q_kernel(const pico_attn_args a, float scale, float scale_log2,
                                                              float* __restrict__ lse2_g, float* __restrict__ delta_g,
                                                              int sq_pad, unsigned long long* __restrict__ stamp_out,
                                                              int nfront, float lse_mul, float lse_pad) {
@@ -329,6 +344,137 @@ __global__ __launch_bounds__(256, QCfg<D>::MINB) void attn_bwd_q_kernel(const pi
       }
     }
   };
+  // The pipelined tile (PIPE): one element pair of a half's softmax per slot (2 fma, 2 exp, 2 mul, 1 cvt_pk of
+  // dS^T), KVP-style sched_barrier fences between slots; every operand read two or more slots before its MFMA.
+  auto tile_p = [&](const char* kb, bool mask, int n0) __attribute__((always_inline)) {
+    static_assert(!PIPE || D == 64, "the pipelined dQ tile is written for D = 64");
+    const char* vb = kb + C::IMG;
+    bf16x8 k0[KS], v0[KS], k1[KS], v1[KS];
+    bf16x8 t0[2][DT], t1[2][DT];
+    unsigned w0[8], w1[8];
+    f32x16 s0, d0, s1, d1;
+    auto vp = [&](const f32x16& sv, const f32x16& dv, int e, unsigned& w) __attribute__((always_inline)) {
+      typedef __attribute__((ext_vector_type(2))) float f32x2;
+      typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+      const float a0 = fast_exp2(__builtin_fmaf(sv[2 * e], scale_log2, nl2)) * dv[2 * e];
+      const float a1 = fast_exp2(__builtin_fmaf(sv[2 * e + 1], scale_log2, nl2)) * dv[2 * e + 1];
+      w = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){a0, a1}, bf16x2));
+    };
+    auto pk4 = [&](const unsigned* w) __attribute__((always_inline)) {
+      typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+      return __builtin_bit_cast(bf16x8, (u32x4){w[0], w[1], w[2], w[3]});
+    };
+    auto minit = [&](int kt) __attribute__((always_inline)) {
+      f32x16 m;
+      if (mask) {
+        const int rel = lim_lane - n0 - 4 * h;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) m[i] = (32 * kt + (i & 3) + 8 * (i >> 2)) <= rel ? 0.f : -INFINITY;
+      } else {
+        m = (f32x16)0.f;
+      }
+      return m;
+    };
+#define QP_SLOT() __builtin_amdgcn_sched_barrier(0)
+    k0[0] = lds_read_b128(kb, ro[0]);
+    k0[1] = lds_read_b128(kb, ro[1]);
+    s0 = minit(0);
+    d0 = ndelta;
+    QP_SLOT();
+    s0 = mfma32(k0[0], qf[0], s0);  // a1
+    k0[2] = lds_read_b128(kb, ro[2]);
+    k0[3] = lds_read_b128(kb, ro[3]);
+    QP_SLOT();
+    s0 = mfma32(k0[1], qf[1], s0);  // a2
+    v0[0] = lds_read_b128(vb, ro[0]);
+    v0[1] = lds_read_b128(vb, ro[1]);
+    QP_SLOT();
+    s0 = mfma32(k0[2], qf[2], s0);  // a3
+    v0[2] = lds_read_b128(vb, ro[2]);
+    v0[3] = lds_read_b128(vb, ro[3]);
+    QP_SLOT();
+    s0 = mfma32(k0[3], qf[3], s0);  // a4
+    k1[0] = lds_read_b128(kb, ro[0] + 32 * RB);
+    k1[1] = lds_read_b128(kb, ro[1] + 32 * RB);
+    QP_SLOT();
+    d0 = mfma32(v0[0], df[0], d0);  // a5
+    k1[2] = lds_read_b128(kb, ro[2] + 32 * RB);
+    k1[3] = lds_read_b128(kb, ro[3] + 32 * RB);
+    QP_SLOT();
+    d0 = mfma32(v0[1], df[1], d0);  // a6
+    v1[0] = lds_read_b128(vb, ro[0] + 32 * RB);
+    v1[1] = lds_read_b128(vb, ro[1] + 32 * RB);
+    QP_SLOT();
+    d0 = mfma32(v0[2], df[2], d0);  // a7
+    v1[2] = lds_read_b128(vb, ro[2] + 32 * RB);
+    v1[3] = lds_read_b128(vb, ro[3] + 32 * RB);
+    QP_SLOT();
+    d0 = mfma32(v0[3], df[3], d0);  // a8
+    s1 = minit(1);
+    d1 = ndelta;
+    QP_SLOT();
+    s1 = mfma32(k1[0], qf[0], s1);  // b1
+    t0[0][0] = tr_pair(kb, tro[0][0], tro[0][1]);
+    QP_SLOT();
+    s1 = mfma32(k1[1], qf[1], s1);  // b2
+    t0[0][1] = tr_pair(kb, tro[1][0], tro[1][1]);
+    QP_SLOT();
+    s1 = mfma32(k1[2], qf[2], s1);  // b3
+    vp(s0, d0, 0, w0[0]);
+    QP_SLOT();
+    s1 = mfma32(k1[3], qf[3], s1);  // b4
+    vp(s0, d0, 1, w0[1]);
+    QP_SLOT();
+    d1 = mfma32(v1[0], df[0], d1);  // b5
+    vp(s0, d0, 2, w0[2]);
+    t0[1][0] = tr_pair(kb + 16 * RB, tro[0][0], tro[0][1]);
+    QP_SLOT();
+    d1 = mfma32(v1[1], df[1], d1);  // b6
+    vp(s0, d0, 3, w0[3]);
+    t0[1][1] = tr_pair(kb + 16 * RB, tro[1][0], tro[1][1]);
+    QP_SLOT();
+    d1 = mfma32(v1[2], df[2], d1);  // b7
+    vp(s0, d0, 4, w0[4]);
+    QP_SLOT();
+    d1 = mfma32(v1[3], df[3], d1);  // b8
+    vp(s0, d0, 5, w0[5]);
+    QP_SLOT();
+    const bf16x8 ds00 = pk4(w0);
+    dq[0] = mfma32(t0[0][0], ds00, dq[0]);  // c1
+    vp(s0, d0, 6, w0[6]);
+    t1[0][0] = tr_pair(kb + 32 * RB, tro[0][0], tro[0][1]);
+    QP_SLOT();
+    dq[1] = mfma32(t0[0][1], ds00, dq[1]);  // c2
+    vp(s0, d0, 7, w0[7]);
+    t1[0][1] = tr_pair(kb + 32 * RB, tro[1][0], tro[1][1]);
+    QP_SLOT();
+    const bf16x8 ds01 = pk4(w0 + 4);
+    dq[0] = mfma32(t0[1][0], ds01, dq[0]);  // c3
+    vp(s1, d1, 0, w1[0]);
+    vp(s1, d1, 1, w1[1]);
+    QP_SLOT();
+    dq[1] = mfma32(t0[1][1], ds01, dq[1]);  // c4
+    vp(s1, d1, 2, w1[2]);
+    vp(s1, d1, 3, w1[3]);
+    t1[1][0] = tr_pair(kb + 48 * RB, tro[0][0], tro[0][1]);
+    t1[1][1] = tr_pair(kb + 48 * RB, tro[1][0], tro[1][1]);
+    QP_SLOT();
+    const bf16x8 ds10 = pk4(w1);
+    dq[0] = mfma32(t1[0][0], ds10, dq[0]);  // d1
+    vp(s1, d1, 4, w1[4]);
+    vp(s1, d1, 5, w1[5]);
+    QP_SLOT();
+    dq[1] = mfma32(t1[0][1], ds10, dq[1]);  // d2
+    vp(s1, d1, 6, w1[6]);
+    vp(s1, d1, 7, w1[7]);
+    QP_SLOT();
+    const bf16x8 ds11 = pk4(w1 + 4);
+    dq[0] = mfma32(t1[1][0], ds11, dq[0]);  // d3
+    QP_SLOT();
+    dq[1] = mfma32(t1[1][1], ds11, dq[1]);  // d4
+    QP_SLOT();
+#undef QP_SLOT
+  };
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // prologue tiles and loads landed
 #if PICO_BWDQ_WGSTAMP
   wgs[1] = __builtin_amdgcn_s_memrealtime();
@@ -341,18 +487,14 @@ __global__ __launch_bounds__(256, QCfg<D>::MINB) void attn_bwd_q_kernel(const pi
       const int t = t0 + u;
       if (t >= ntiles) break;
       if (t > 0) {  // tile t landed (this wave's pieces); the younger tiles stay in flight
-        if (P == 2 && t + 1 < ntiles) {
-          if constexpr (C::NPW == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-          else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        } else {
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
+        wait_vmcnt(min(P - 1, ntiles - 1 - t) * C::NPW);  // issued tiles after t stay in flight
       }
       lds_barrier();  // every wave's pieces of tile t visible; slot (t + P) % NBUF no longer read
       if (t + P < ntiles) issue(t + P, (u + P) % C::NBUF);
       const int n0 = t * KT;
       if (n0 <= lim_last) {  // wave-uniform: some row of the wave sees some key of the tile
-        tile(smem + u * C::SLOT, n0 + KT - 1 > lim_first, n0);
+        if constexpr (PIPE) tile_p(smem + u * C::SLOT, n0 + KT - 1 > lim_first, n0);
+        else tile(smem + u * C::SLOT, n0 + KT - 1 > lim_first, n0);
       }
     }
   }
@@ -715,11 +857,16 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kv_kernel(const pico_
       if (t >= ntiles) break;
       if (t > 0) {
         // this wave's pieces of tile t landed; the next tile's may stay in flight
-        if (t + 2 <= ntiles) {
-          if (wave < C::NP % KNW) wait_vmcnt(NPMY_LO + 1);
-          else wait_vmcnt(NPMY_LO);
+        if constexpr (C::PD == 2) {
+          if (t + 2 <= ntiles) {  // this wave's pieces of tile t landed; the next tile's may stay in flight
+            if (wave < C::NP % KNW) wait_vmcnt(NPMY_LO + 1);
+            else wait_vmcnt(NPMY_LO);
+          } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          }
         } else {
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          const int younger = min(C::PD - 1, ntiles - 1 - t);  // issued tiles after t (still in flight)
+          wait_vmcnt(younger * (wave < C::NP % KNW ? NPMY_LO + 1 : NPMY_LO));
         }
         lds_barrier();  // everyone's pieces visible; the slot of tile t - 1 is no longer read
       }
@@ -851,7 +998,10 @@ struct KVPCfg {
   static constexpr int QIMG = QT2 * RB;          // one Q (or dO) 64-row image, 8 KiB
   static constexpr int LSD = 1024;               // -LSE/scale [64] | -delta [64] (+ 512 B the DMA piece repeats)
   static constexpr int SLOT = 2 * QIMG + LSD;    // 17 KiB; 3 slots = 51 KiB per workgroup
-  static constexpr int NBUF = 3, PD = 2;
+#ifndef PICO_KVP_NBUF
+#define PICO_KVP_NBUF 3
+#endif
+  static constexpr int NBUF = PICO_KVP_NBUF, PD = NBUF - 1;  // ring slots, prefetch distance (tiles)
   static constexpr int RPP = 1024 / RB;          // 8 image rows per 1-KiB piece
   static constexpr int NQP = QIMG / 1024;        // 8 pieces per image
   static constexpr int NP = 2 * NQP + 1;         // 17 pieces per tile: 4 per wave + wave 0's LSE / delta piece
@@ -864,8 +1014,20 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kvp_kernel(const pico
                                                                 const float* __restrict__ sinit_g,
                                                                 const float* __restrict__ delta_g, int sq_pad,
                                                                 int hsplit, float* __restrict__ dkv_part,
-                                                                const BlkGroups grp) {
+                                                                const BlkGroups grp,
+                                                                unsigned long long* __restrict__ stamp_out) {
   using C = KVPCfg;
+#if PICO_KVP_STAMP
+  unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tlast = 0;
+#define KVP_ST(i)                                          \
+  {                                                        \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+    ph[i] += t_ - tlast;                                   \
+    tlast = t_;                                            \
+  }
+#else
+#define KVP_ST(i)
+#endif
   constexpr int KS = C::KS, DT = C::DT, CPR = C::CPR, RB = C::RB;
   static_assert(C::NP == 4 * KNW + 1, "four Q / dO pieces per wave + one LSE / delta piece");
   __shared__ __attribute__((aligned(16))) char smem[C::NBUF * C::SLOT];
@@ -1033,18 +1195,22 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kvp_kernel(const pico
     for (int u = 0; u < C::NBUF; ++u) {
       const int t = t0 + u;
       if (t >= ntiles) break;
+#if PICO_KVP_STAMP
+      tlast = __builtin_amdgcn_s_memtime();
+      ph[7] += 1;
+#endif
       if (t > 0) {
-        if (t + 2 <= ntiles) {  // tile t + 1 stays in flight
-          if (wave == 0) wait_vmcnt(5);
-          else wait_vmcnt(4);
-        } else {
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
+        // this wave's pieces of tile t landed; those of the younger tiles already issued stay in flight
+        const int younger = min(C::PD - 1, ntiles - 1 - t);
+        wait_vmcnt(younger * (wave == 0 ? 5 : 4));
+        KVP_ST(0);
         lds_barrier();  // every wave's pieces of tile t visible; the slot of tile t - 1 is no longer read
+        KVP_ST(1);
       }
       if (t + C::PD < ntiles) issue((u + C::PD) % C::NBUF, nxt);
       advance(nxt);
       KVP_SLOT();
+      KVP_ST(2);
       const char* qs = smem + u * C::SLOT;
       const char* dos = qs + C::QIMG;
       const float* lsd = (const float*)(qs + 2 * C::QIMG);
@@ -1111,6 +1277,7 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kvp_kernel(const pico
       db[0] = lds_read_b128(dos, qo[0] + 32 * RB);
       db[1] = lds_read_b128(dos, qo[1] + 32 * RB);
       KVP_SLOT();
+      KVP_ST(3);
       sB = mfma32(qb[0], kf[0], sB);  // b1
       db[2] = lds_read_b128(dos, qo[2] + 32 * RB);
       db[3] = lds_read_b128(dos, qo[3] + 32 * RB);
@@ -1142,6 +1309,7 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kvp_kernel(const pico
       vpair(sA, dpA, 5, pwA[5], swA[5]);
       toA[1][1] = tr_pair(dos + 16 * RB, tro[1][0], tro[1][1]);
       KVP_SLOT();
+      KVP_ST(4);
       const bf16x8 pA0 = pk4(pwA), sA0 = pk4(swA);
       dv[0] = mfma32(toA[0][0], pA0, dv[0]);  // c1
       vpair(sA, dpA, 6, pwA[6], swA[6]);
@@ -1176,6 +1344,7 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kvp_kernel(const pico
       vpair(sB, dpB, 5, pwB[5], swB[5]);
       toB[1][1] = tr_pair(dos + 48 * RB, tro[1][0], tro[1][1]);
       KVP_SLOT();
+      KVP_ST(5);
       const bf16x8 pB0 = pk4(pwB), sB0 = pk4(swB);
       dv[0] = mfma32(toB[0][0], pB0, dv[0]);  // d1
       vpair(sB, dpB, 6, pwB[6], swB[6]);
@@ -1197,6 +1366,7 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kvp_kernel(const pico
       KVP_SLOT();
       dk[1] = mfma32(tqB[1][1], sB1, dk[1]);  // d8
       KVP_SLOT();
+      KVP_ST(6);
       q0cur = q0cur + QT2 >= qend ? qstart : q0cur + QT2;
     }
   }
@@ -1248,8 +1418,20 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kvp_kernel(const pico
     }
   }
   }  // key blocks of the group
+#if PICO_KVP_STAMP
+  if ((threadIdx.x & 63) == 0 && blockIdx.x < 16384) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) stamp_out[((int64_t)blockIdx.x * 4 + wave) * 8 + i] = ph[i];
+  }
+#endif
 }
+#undef KVP_ST
 #undef KVP_SLOT
+
+bool qp_enabled() {
+  const char* e = getenv("PICO_ATTN_QP");
+  return e && e[0] == '1';
+}
 
 bool kvp_enabled() {
   const char* e = getenv("PICO_ATTN_KVP");
@@ -1299,8 +1481,11 @@ int q_front(const pico_attn_args* a) {
   if (!a->causal) return 0;
   const int nmb = (int)((a->seqlen_q + QB - 1) / QB);
   const int64_t nbh = a->batch * a->heads_q;
-  const int64_t first = (int64_t)pico_num_cus() * (a->head_dim == 64 ? QCfg<64>::MINB : QCfg<128>::MINB) /
-                        (nbh > 0 ? nbh : 1);  // groups resident at once
+  int minb = a->head_dim == 64 ? QCfg<64>::MINB : QCfg<128>::MINB;
+#ifndef PICO_SPLIT_D128_TU
+  if (a->head_dim == 64 && qp_enabled()) minb = 2;  // the pipelined tile: two workgroups per CU
+#endif
+  const int64_t first = (int64_t)pico_num_cus() * minb / (nbh > 0 ? nbh : 1);  // groups resident at once
   return first < nmb ? (int)(nmb - first) : 0;
 }
 
@@ -1382,6 +1567,14 @@ int launch_split(const pico_attn_args* a, hipStream_t s) {
   const int nmb = (int)((a->seqlen_q + QB - 1) / QB);
   const int64_t gq = (int64_t)nmb * a->batch * a->heads_q;
   PICO_REQUIRE(gq < (1ll << 31), "pico_attn_bwd: grid too large");
+#ifndef PICO_SPLIT_D128_TU
+  if (D == 64 && qp_enabled())
+    PICO_TRY(pico_launch(PICO_K_ATTN_BWD_Q, "attn_bwd_q", attn_bwd_q_kernel<D, CAUSAL, true>, dim3((int)gq), dim3(256), 0, s,
+                         *a, a->softmax_scale, sl2, lse2, delta, sq_pad,
+                         (unsigned long long*)((char*)a->workspace + pico_attn_bwd_split_workspace(a) - STAMP_BYTES),
+                         q_front(a), use_kvp ? -1.0f / a->softmax_scale : LOG2E, use_kvp ? -INFINITY : INFINITY));
+  else
+#endif
   PICO_TRY(pico_launch(PICO_K_ATTN_BWD_Q, "attn_bwd_q", attn_bwd_q_kernel<D, CAUSAL>, dim3((int)gq), dim3(256), 0, s,
                        *a, a->softmax_scale, sl2, lse2, delta, sq_pad,
                        (unsigned long long*)((char*)a->workspace + pico_attn_bwd_split_workspace(a) - STAMP_BYTES),
@@ -1395,7 +1588,8 @@ int launch_split(const pico_attn_args* a, hipStream_t s) {
 #ifndef PICO_SPLIT_D128_TU
   if (use_kvp) {
     PICO_TRY(pico_launch(PICO_K_ATTN_BWD_KV, "attn_bwd_kv", attn_bwd_kvp_kernel<CAUSAL, 2>, dim3((int)nblk),
-                         dim3(KNW * 64), 0, s, *a, a->softmax_scale, sl2, lse2, delta, sq_pad, hsplit, dkv_part, kg));
+                         dim3(KNW * 64), 0, s, *a, a->softmax_scale, sl2, lse2, delta, sq_pad, hsplit, dkv_part, kg,
+                         stamps));
   } else
 #endif
   if constexpr (D == 128) {

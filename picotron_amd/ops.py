@@ -378,6 +378,27 @@ def wgrad_accumulate(params, dy2, x2):
             torch.addmm(mg, dy2.t(), x2, beta=sc, alpha=sc, out_dtype=torch.float32, out=mg)
             p._pico_wgrad_ready()
             return (None,)
+    if len(params) > 1 and all(getattr(p, "_pico_wgrad_ready", None) is not None and
+                               getattr(p, "main_grad", None) is not None and p.main_grad.dtype == torch.float32 and
+                               p.main_grad.is_contiguous() and tuple(p.main_grad.shape) == tuple(p.shape) and
+                               p.dtype == dy2.dtype for p in params):
+        # Row-stacked parameters (q|k|v, gate|up) under DataParallelBucket: their main_grads sit in different
+        # buckets (not one fp32 block), so one GEMM cannot accumulate into them. The reference's sequence — the
+        # bf16 dW, then the bucket hook's main_grad += dW (x 1/W when syncing) — runs here, with the same kernels
+        # and the same values, instead of through autograd: an AccumulateGrad node is created on the stream of
+        # the forward that first uses the parameter, so in the two-stream pipelined graph (forward i + 1 beside
+        # backward i) the node of micro-batch i served micro-batch i + 1 too, and torch synchronised the two
+        # streams on every such gradient ("AccumulateGrad node's stream does not match ...").
+        from .data_parallel.bucket import get_kernels
+        buf = torch.mm(dy2.t(), x2)
+        r0 = 0
+        for p in params:
+            n = p.shape[0]
+            sync, world = p._pico_wgrad_sync()
+            get_kernels().accumulate(p.main_grad, buf[r0:r0 + n], world if sync else 1)
+            p._pico_wgrad_ready()
+            r0 += n
+        return (None,) * len(params)
     if all(p.dtype == dy2.dtype and getattr(p, "main_grad", None) is None and not _has_hooks(p) for p in params):
         grads = [p.grad for p in params]
         if all(g is None for g in grads):
@@ -402,6 +423,15 @@ def wgrad_accumulate(params, dy2, x2):
             if ok:
                 buf = torch.as_strided(base, (nrows, K), (K, 1))
                 torch.addmm(buf, dy2.t(), x2, out=buf)
+                return (None,) * len(params)
+            if all(g.dtype == dy2.dtype and g.shape == p.shape for p, g in zip(params, grads)):
+                # separately allocated gradients (a caller's own zeros_like per parameter): AccumulateGrad's in-place
+                # `grad += dW` done here (same values), not through autograd — see the DP branch above for why
+                buf = torch.mm(dy2.t(), x2)
+                r0 = 0
+                for p, g in zip(params, grads):
+                    g.add_(buf[r0:r0 + p.shape[0]].view(p.shape))
+                    r0 += p.shape[0]
                 return (None,) * len(params)
     return _plain_grads(params, torch.mm(dy2.t(), x2))
 

@@ -7,6 +7,7 @@ import socket
 from types import SimpleNamespace
 
 import pytest
+from conftest import ROOT
 import torch
 
 pytestmark = pytest.mark.gpu
@@ -606,6 +607,28 @@ def test_bench_dp2_gloo_on_one_gpu():
     assert math.isfinite(out["loss_last"]) and out["loss_last"] < math.log(49152) + 0.1
     ar = out["allreduce"]
     assert ar["buckets"] > 0 and ar["bytes"] > 0 and ar["busbw_GBps"] > 0
+    # the step's exposed all-reduce: measured per timed step, plus the W = 8 model
+    assert ar["exposed_ms"] >= 0 and len(ar["bucket_ready_ms"]) == ar["buckets"]
+    assert set(ar["model_exposed_ms"]) == {"300.0", "600.0", "1071.0"}
+
+
+def test_bench_dp_bucket_grad_acc1_rccl():
+    """bench.py --dp-bucket at one rank over RCCL with grad_acc 1 (the only micro-batch is the eager
+    syncing one, so the pipelined graph never runs and take_loss has nothing to hand back): the step runs, the loss is
+    finite, and the N > 1 exposure object is reported from the one syncing backward per step."""
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(HSA_ENABLE_IPC_MODE_LEGACY="0", MASTER_PORT=str(_free_port()))
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--dp-bucket", "--layers", "2", "--grad-acc", "1",
+           "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--no-kernel-timing"]
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    out = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
+    assert math.isfinite(out["loss_last"]) and out["config"]["grad_acc"] == 1
+    ar = out["allreduce"]
+    assert ar["exposed_ms"] >= 0 and ar["buckets"] == len(ar["bucket_bytes"])
 
 
 def test_smollm_step_pipelined_paired_matches_eager(monkeypatch):
@@ -647,3 +670,20 @@ def test_smollm_step_pipelined_paired_matches_eager(monkeypatch):
     finally:
         pgm.process_group_manager = None
         dist.destroy_process_group()
+
+
+def test_pipelined_graph_no_accumulategrad_stream_sync():
+    """in the two-stream pipelined graph (forward i + 1 beside backward i) no gradient may reach
+    autograd's AccumulateGrad node across streams (torch then synchronises the two streams on it). Every weight
+    gradient is accumulated by its producer instead (ops.wgrad_accumulate: the fused GEMM, the in-place add into
+    separately allocated gradients, the DP bucket's accumulate kernel for row-stacked parameters). One fresh process
+    per set-up (torch warns once per process): bench.py's gradient layout, per-parameter zeros, DataParallelBucket."""
+    import subprocess
+    import sys
+    for setup in ("bench", "zeros", "dp"):
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "accgrad_warn_probe.py"), setup],
+                           capture_output=True, text=True, timeout=300, env=dict(os.environ, PROBE_PORT=str(_free_port())))
+        line = [l for l in r.stdout.splitlines() if l.startswith("ACCGRAD_STREAM_WARNINGS")]
+        assert r.returncode == 0 and line, (setup, r.returncode, r.stdout[-2000:], r.stderr[-3000:])
+        print(line[0], flush=True)
+        assert line[0].split()[-1] == "0", line[0]
