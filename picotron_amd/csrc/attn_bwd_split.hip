@@ -226,20 +226,24 @@ __global__ __launch_bounds__(256, PIPE ? 2 : QCfg<D>::MINB) void attn_bwd_q_kern
   const int64_t kst = (int64_t)KT * ksd * 2, vst = (int64_t)KT * vsd * 2;
   const char* kp_nxt = (const char*)kg;
   const char* vp_nxt = (const char*)vg;
-  auto issue = [&](int tile, int slot_i) __attribute__((always_inline)) {
+  auto issue_piece = [&](int tile, int slot_i, int i) __attribute__((always_inline)) {
     const unsigned slot = smem_lds + (unsigned)slot_i * (unsigned)C::SLOT;
     const int base = tile * KT;
     const int lastrow = Sk - 1 - base;  // rows past it are clamped (finite; masked by the softmax)
     const bool full = base + KT <= Sk;
-#pragma unroll
-    for (int i = 0; i < C::NPW; ++i) {
-      const char* tb = is_k[i] ? kp_nxt : vp_nxt;
-      const unsigned off = full ? full_off[i]
-                                : (unsigned)(min(src_row[i], lastrow) * (is_k[i] ? ksd : vsd) + src_col[i]) * 2u;
-      dma_piece(tb, off, slot + dst_off[i]);
-    }
+    const char* tb = is_k[i] ? kp_nxt : vp_nxt;
+    const unsigned off = full ? full_off[i]
+                              : (unsigned)(min(src_row[i], lastrow) * (is_k[i] ? ksd : vsd) + src_col[i]) * 2u;
+    dma_piece(tb, off, slot + dst_off[i]);
+  };
+  auto bump = [&]() __attribute__((always_inline)) {
     kp_nxt += kst;
     vp_nxt += vst;
+  };
+  auto issue = [&](int tile, int slot_i) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < C::NPW; ++i) issue_piece(tile, slot_i, i);
+    bump();
   };
   constexpr int P = C::NBUF - 1;  // prefetch distance
 #pragma unroll
@@ -346,7 +350,7 @@ __global__ __launch_bounds__(256, PIPE ? 2 : QCfg<D>::MINB) void attn_bwd_q_kern
   };
   // The pipelined tile (PIPE): one element pair of a half's softmax per slot (2 fma, 2 exp, 2 mul, 1 cvt_pk of
   // dS^T), KVP-style sched_barrier fences between slots; every operand read two or more slots before its MFMA.
-  auto tile_p = [&](const char* kb, bool mask, int n0) __attribute__((always_inline)) {
+  auto tile_p = [&](const char* kb, bool mask, int n0, int dtile, int dslot) __attribute__((always_inline)) {
     static_assert(!PIPE || D == 64, "the pipelined dQ tile is written for D = 64");
     const char* vb = kb + C::IMG;
     bf16x8 k0[KS], v0[KS], k1[KS], v1[KS];
@@ -463,15 +467,22 @@ __global__ __launch_bounds__(256, PIPE ? 2 : QCfg<D>::MINB) void attn_bwd_q_kern
     dq[0] = mfma32(t1[0][0], ds10, dq[0]);  // d1
     vp(s1, d1, 4, w1[4]);
     vp(s1, d1, 5, w1[5]);
+    if (dtile >= 0) issue_piece(dtile, dslot, 0);
     QP_SLOT();
     dq[1] = mfma32(t1[0][1], ds10, dq[1]);  // d2
     vp(s1, d1, 6, w1[6]);
     vp(s1, d1, 7, w1[7]);
+    if (dtile >= 0) issue_piece(dtile, dslot, 1);
     QP_SLOT();
     const bf16x8 ds11 = pk4(w1 + 4);
     dq[0] = mfma32(t1[1][0], ds11, dq[0]);  // d3
+    if (dtile >= 0) issue_piece(dtile, dslot, 2);
     QP_SLOT();
     dq[1] = mfma32(t1[1][1], ds11, dq[1]);  // d4
+    if (dtile >= 0) {
+      issue_piece(dtile, dslot, 3);
+      bump();
+    }
     QP_SLOT();
 #undef QP_SLOT
   };
@@ -490,11 +501,15 @@ __global__ __launch_bounds__(256, PIPE ? 2 : QCfg<D>::MINB) void attn_bwd_q_kern
         wait_vmcnt(min(P - 1, ntiles - 1 - t) * C::NPW);  // issued tiles after t stay in flight
       }
       lds_barrier();  // every wave's pieces of tile t visible; slot (t + P) % NBUF no longer read
-      if (t + P < ntiles) issue(t + P, (u + P) % C::NBUF);
       const int n0 = t * KT;
-      if (n0 <= lim_last) {  // wave-uniform: some row of the wave sees some key of the tile
-        if constexpr (PIPE) tile_p(smem + u * C::SLOT, n0 + KT - 1 > lim_first, n0);
-        else tile(smem + u * C::SLOT, n0 + KT - 1 > lim_first, n0);
+      const bool busy = n0 <= lim_last;  // wave-uniform: some row of the wave sees some key of the tile
+      if constexpr (PIPE) {
+        // the pipelined tile issues the DMA of tile t + P in its M2 gaps (one piece per slot; see tile_p)
+        if (t + P < ntiles && !busy) issue(t + P, (u + P) % C::NBUF);
+        if (busy) tile_p(smem + u * C::SLOT, n0 + KT - 1 > lim_first, n0, t + P < ntiles ? t + P : -1, (u + P) % C::NBUF);
+      } else {
+        if (t + P < ntiles) issue(t + P, (u + P) % C::NBUF);
+        if (busy) tile(smem + u * C::SLOT, n0 + KT - 1 > lim_first, n0);
       }
     }
   }
@@ -1001,6 +1016,9 @@ struct KVPCfg {
 #ifndef PICO_KVP_NBUF
 #define PICO_KVP_NBUF 3
 #endif
+#ifndef PICO_KVP_DMA_FRONT  // 1: the tile's DMA issued right after the barrier (as the 32-row kernel), not in M2(B)
+#define PICO_KVP_DMA_FRONT 0
+#endif
   static constexpr int NBUF = PICO_KVP_NBUF, PD = NBUF - 1;  // ring slots, prefetch distance (tiles)
   static constexpr int RPP = 1024 / RB;          // 8 image rows per 1-KiB piece
   static constexpr int NQP = QIMG / 1024;        // 8 pieces per image
@@ -1018,7 +1036,9 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kvp_kernel(const pico
                                                                 unsigned long long* __restrict__ stamp_out) {
   using C = KVPCfg;
 #if PICO_KVP_STAMP
-  unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tlast = 0;
+  unsigned long long ph[16] = {0}, tlast = 0, tblk = 0;
+  ph[10] = __builtin_amdgcn_s_memrealtime();
+  ph[12] = __builtin_amdgcn_s_memtime();
 #define KVP_ST(i)                                          \
   {                                                        \
     const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
@@ -1049,6 +1069,9 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kvp_kernel(const pico
   const unsigned ring_lds = (unsigned)__builtin_amdgcn_readfirstlane((int)lds_addr(smem));
 #pragma clang loop unroll(disable)
   for (int jb = 0; jb < nblk_wg; ++jb) {
+#if PICO_KVP_STAMP
+  tblk = __builtin_amdgcn_s_memtime();
+#endif
   const int kb = grp.n ? (int)((gw >> (8 * jb)) & 255u) : gi;
   if (jb > 0) lds_barrier();
   int lane_l = lane0;
@@ -1104,10 +1127,10 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kvp_kernel(const pico
     }
   };
   const bool ragged = Sq % QT2 != 0;
-  auto issue = [&](int si, const Tc& c) __attribute__((always_inline)) {
+  // one of this wave's pieces of a tile: i < 4 the image pieces, i == 4 the LSE / delta piece (wave 0 only)
+  auto issue_piece = [&](int si, const Tc& c, int i) __attribute__((always_inline)) {
     const unsigned dst = ring_lds + (unsigned)si * (unsigned)C::SLOT;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    if (i < 4) {
       const int jj = (wave + 4 * i) % C::NQP;
       unsigned off = pc_off[i];
       if (ragged && c.q0 + QT2 > Sq) {  // partial tile: rows past Sq - 1 clamped (finite; their LSE is +inf)
@@ -1118,13 +1141,16 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kvp_kernel(const pico
                          8 * (((l2 & 63) % CPR) ^ swz<64>(row)) * 2);
       }
       dma_piece(i < 2 ? c.qp : c.dp, off, dst + (i < 2 ? 0u : (unsigned)C::QIMG) + (unsigned)jj * 1024u);
-    }
-    if (wave == 0) {
+    } else if (wave == 0) {
       int l = lane0;
       asm volatile("" : "+v"(l));
       l &= 31;
       dma_piece(c.lp, (unsigned)(16 * (l & 15)) + ((l >> 4) ? delta_off : 0u), dst + 2u * C::QIMG);
     }
+  };
+  auto issue = [&](int si, const Tc& c) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < 5; ++i) issue_piece(si, c, i);
   };
   Tc nxt = make_tc(hq0, q00);
 #pragma unroll
@@ -1189,6 +1215,9 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kvp_kernel(const pico
 #pragma unroll
     for (int i = 0; i < 16; ++i) s[i] = ((i & 3) + 8 * (i >> 2) < rel) ? -INFINITY : s[i];
   };
+#if PICO_KVP_STAMP
+  ph[8] += __builtin_amdgcn_s_memtime() - tblk;  // prologue of this block
+#endif
   int q0cur = q00;
   for (int t0 = 0; t0 < ntiles; t0 += C::NBUF) {
 #pragma unroll
@@ -1207,8 +1236,14 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kvp_kernel(const pico
         lds_barrier();  // every wave's pieces of tile t visible; the slot of tile t - 1 is no longer read
         KVP_ST(1);
       }
-      if (t + C::PD < ntiles) issue((u + C::PD) % C::NBUF, nxt);
-      advance(nxt);
+      // the DMA of tile t + PD is issued in the gaps of this tile's last MFMA phase (M2(B)), one piece per slot:
+      // an LDS-DMA instruction stalls its wave ~90 cycles at issue (stamps: 462 cycles per tile for the five
+      // pieces issued back to back after the barrier); behind an MFMA that stall runs under the matrix pipe
+      const bool dma_next = t + C::PD < ntiles;
+      const int DSLOT = (u + C::PD) % C::NBUF;  // a constant after unrolling
+#if PICO_KVP_DMA_FRONT
+      if (dma_next) issue(DSLOT, nxt);
+#endif
       KVP_SLOT();
       KVP_ST(2);
       const char* qs = smem + u * C::SLOT;
@@ -1354,22 +1389,41 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kvp_kernel(const pico
       vpair(sB, dpB, 7, pwB[7], swB[7]);
       KVP_SLOT();
       dv[1] = mfma32(toB[0][1], pB0, dv[1]);  // d3
+#if !PICO_KVP_DMA_FRONT
+      if (dma_next) issue_piece(DSLOT, nxt, 0);
+#endif
       KVP_SLOT();
       dk[1] = mfma32(tqB[0][1], sB0, dk[1]);  // d4
+#if !PICO_KVP_DMA_FRONT
+      if (dma_next) issue_piece(DSLOT, nxt, 1);
+#endif
       KVP_SLOT();
       const bf16x8 pB1 = pk4(pwB + 4), sB1 = pk4(swB + 4);
       dv[0] = mfma32(toB[1][0], pB1, dv[0]);  // d5
+#if !PICO_KVP_DMA_FRONT
+      if (dma_next) issue_piece(DSLOT, nxt, 2);
+#endif
       KVP_SLOT();
       dk[0] = mfma32(tqB[1][0], sB1, dk[0]);  // d6
+#if !PICO_KVP_DMA_FRONT
+      if (dma_next) issue_piece(DSLOT, nxt, 3);
+#endif
       KVP_SLOT();
       dv[1] = mfma32(toB[1][1], pB1, dv[1]);  // d7
+#if !PICO_KVP_DMA_FRONT
+      if (dma_next) issue_piece(DSLOT, nxt, 4);
+#endif
       KVP_SLOT();
       dk[1] = mfma32(tqB[1][1], sB1, dk[1]);  // d8
+      advance(nxt);
       KVP_SLOT();
       KVP_ST(6);
       q0cur = q0cur + QT2 >= qend ? qstart : q0cur + QT2;
     }
   }
+#if PICO_KVP_STAMP
+  tblk = __builtin_amdgcn_s_memtime();
+#endif
 
   // ---- epilogue (as attn_bwd_kv_kernel): lane = key kw + r, register i of tile dt = d 32 dt + acc_row(i, h) ----
   if (hsplit == 1) {
@@ -1417,11 +1471,17 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kvp_kernel(const pico
         }
     }
   }
+#if PICO_KVP_STAMP
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  ph[9] += __builtin_amdgcn_s_memtime() - tblk;  // epilogue of this block (stores drained)
+#endif
   }  // key blocks of the group
 #if PICO_KVP_STAMP
-  if ((threadIdx.x & 63) == 0 && blockIdx.x < 16384) {
+  ph[11] = __builtin_amdgcn_s_memrealtime();
+  ph[13] = __builtin_amdgcn_s_memtime();
+  if ((threadIdx.x & 63) == 0 && blockIdx.x < 8192) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) stamp_out[((int64_t)blockIdx.x * 4 + wave) * 8 + i] = ph[i];
+    for (int i = 0; i < 16; ++i) stamp_out[((int64_t)blockIdx.x * 4 + wave) * 16 + i] = ph[i];
   }
 #endif
 }

@@ -41,15 +41,34 @@ def main():
         ws[nbytes - 65536 * 4 * 8:].zero_()
         L.check(lib.pico_attn_bwd(ctypes.byref(a), L.stream_of(q)), "bwd")
     torch.cuda.synchronize()
-    st = ws[nbytes - 65536 * 4 * 8:].cpu().numpy().view(np.uint64).astype(np.float64).reshape(-1, 4, 8)
+    st = ws[nbytes - 65536 * 4 * 8:].cpu().numpy().view(np.uint64).astype(np.float64).reshape(-1, 4, 16)
     live = st[:, 0, 7] > 0
     st = st[live]
     nwg = st.shape[0]
+    rt0, rt1 = st[:, :, 10], st[:, :, 11]  # s_memrealtime, 100 MHz
+    clk = (st[:, :, 13] - st[:, :, 12]) / ((rt1 - rt0) / 100e6) / 1e9  # GHz per wave
+    t0 = rt0.min()
+    life_us = (rt1 - rt0) / 100.0
     tiles = st[:, :, 7:8]
     per_tile = st[:, :, :7] / np.maximum(tiles, 1)
     out = {"workgroups": int(nwg), "tiles_per_wave_mean": round(float(tiles.mean()), 2),
            "cycles_per_tile": {p: round(float((st[:, :, i].sum()) / tiles.sum()), 1) for i, p in enumerate(PHASES)}}
     out["cycles_per_tile"]["total"] = round(float(st[:, :, :7].sum() / tiles.sum()), 1)
+    span = (rt1.max() - t0) / 100.0
+    loop_cyc = st[:, :, :7].sum(axis=2)
+    out["span_us"] = round(float(span), 2)
+    out["clock_GHz_median"] = round(float(np.median(clk)), 3)
+    out["wave_life_us_mean"] = round(float(life_us.mean()), 2)
+    out["wave_life_us_max"] = round(float(life_us.max()), 2)
+    # shares of a wave's lifetime (cycles): the tile loop, the blocks' prologues and epilogues, the rest (the
+    # group's block switches, the kernel entry before the first block)
+    life_cyc = st[:, :, 13] - st[:, :, 12]
+    out["share_of_wave_life"] = {"loop": round(float(loop_cyc.sum() / life_cyc.sum()), 3),
+                                 "prologue": round(float(st[:, :, 8].sum() / life_cyc.sum()), 3),
+                                 "epilogue": round(float(st[:, :, 9].sum() / life_cyc.sum()), 3)}
+    out["prologue_us_per_wave_mean"] = round(float((st[:, :, 8] / np.maximum(clk, 1e-3) / 1e3).mean()), 2)
+    ends = (rt1.max(axis=1) - t0) / 100.0
+    out["wg_end_us_percentiles"] = [round(float(np.percentile(ends, p)), 2) for p in (0, 10, 50, 90, 100)]
     nbh = B * H
     cus = 256
     cls = (np.arange(nwg) // nbh) * nbh // cus
