@@ -1019,6 +1019,9 @@ struct KVPCfg {
 #ifndef PICO_KVP_DMA_FRONT  // 1: the tile's DMA issued right after the barrier (as the 32-row kernel), not in M2(B)
 #define PICO_KVP_DMA_FRONT 0
 #endif
+#ifndef PICO_KVP_STAGE  // 1: register-staged tiles (global_load_dwordx4 after the barrier, ds_write_b128 after M2(B))
+#define PICO_KVP_STAGE 0  //    instead of LDS-DMA
+#endif
   static constexpr int NBUF = PICO_KVP_NBUF, PD = NBUF - 1;  // ring slots, prefetch distance (tiles)
   static constexpr int RPP = 1024 / RB;          // 8 image rows per 1-KiB piece
   static constexpr int NQP = QIMG / 1024;        // 8 pieces per image
@@ -1152,10 +1155,50 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kvp_kernel(const pico
 #pragma unroll
     for (int i = 0; i < 5; ++i) issue_piece(si, c, i);
   };
+#if PICO_KVP_STAGE
+  // register-staged form: this wave's pieces of a tile as plain 16-B loads (the swizzle goes on the LDS address)
+  typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+  u32x4 stg[5];
+  auto stage_load = [&](const Tc& c) __attribute__((always_inline)) {
+    int l2 = lane0;
+    asm volatile("" : "+v"(l2));
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int jj = (wave + 4 * i) % C::NQP;
+      const int row = C::RPP * jj + (l2 & 63) / CPR;
+      const int rr = (ragged && c.q0 + QT2 > Sq) ? min(c.q0 + row, Sq - 1) - c.q0 : row;
+      const char* src = (i < 2 ? c.qp : c.dp) + (int64_t)rr * (i < 2 ? qs1 : ds1) + ((l2 & 63) % CPR) * 16;
+      stg[i] = *reinterpret_cast<const u32x4*>(src);
+    }
+    if (wave == 0) {
+      const int l = l2 & 31;
+      stg[4] = *reinterpret_cast<const u32x4*>(c.lp + 16 * (l & 15) + ((l >> 4) ? delta_off : 0u));
+    }
+  };
+  auto stage_store = [&](int si) __attribute__((always_inline)) {
+    int l2 = lane0;
+    asm volatile("" : "+v"(l2));
+    char* dst = smem + si * C::SLOT;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int jj = (wave + 4 * i) % C::NQP;
+      const int row = C::RPP * jj + (l2 & 63) / CPR;
+      *reinterpret_cast<u32x4*>(dst + (i < 2 ? 0 : C::QIMG) + lds_off<64>(row, (l2 & 63) % CPR)) = stg[i];
+    }
+    if (wave == 0) *reinterpret_cast<u32x4*>(dst + 2 * C::QIMG + 16 * (l2 & 63)) = stg[4];
+  };
+#endif
   Tc nxt = make_tc(hq0, q00);
 #pragma unroll
   for (int j = 0; j < C::PD; ++j) {
+#if PICO_KVP_STAGE
+    if (j < ntiles) {
+      stage_load(nxt);
+      stage_store(j);
+    }
+#else
     if (j < ntiles) issue(j, nxt);
+#endif
     advance(nxt);
   }
 
@@ -1229,9 +1272,11 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kvp_kernel(const pico
       ph[7] += 1;
 #endif
       if (t > 0) {
+#if !PICO_KVP_STAGE
         // this wave's pieces of tile t landed; those of the younger tiles already issued stay in flight
         const int younger = min(C::PD - 1, ntiles - 1 - t);
         wait_vmcnt(younger * (wave == 0 ? 5 : 4));
+#endif
         KVP_ST(0);
         lds_barrier();  // every wave's pieces of tile t visible; the slot of tile t - 1 is no longer read
         KVP_ST(1);
@@ -1241,7 +1286,9 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kvp_kernel(const pico
       // pieces issued back to back after the barrier); behind an MFMA that stall runs under the matrix pipe
       const bool dma_next = t + C::PD < ntiles;
       const int DSLOT = (u + C::PD) % C::NBUF;  // a constant after unrolling
-#if PICO_KVP_DMA_FRONT
+#if PICO_KVP_STAGE
+      if (dma_next) stage_load(nxt);  // written into slot DSLOT after M2(B)
+#elif PICO_KVP_DMA_FRONT
       if (dma_next) issue(DSLOT, nxt);
 #endif
       KVP_SLOT();
@@ -1389,32 +1436,35 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kvp_kernel(const pico
       vpair(sB, dpB, 7, pwB[7], swB[7]);
       KVP_SLOT();
       dv[1] = mfma32(toB[0][1], pB0, dv[1]);  // d3
-#if !PICO_KVP_DMA_FRONT
+#if !PICO_KVP_DMA_FRONT && !PICO_KVP_STAGE
       if (dma_next) issue_piece(DSLOT, nxt, 0);
 #endif
       KVP_SLOT();
       dk[1] = mfma32(tqB[0][1], sB0, dk[1]);  // d4
-#if !PICO_KVP_DMA_FRONT
+#if !PICO_KVP_DMA_FRONT && !PICO_KVP_STAGE
       if (dma_next) issue_piece(DSLOT, nxt, 1);
 #endif
       KVP_SLOT();
       const bf16x8 pB1 = pk4(pwB + 4), sB1 = pk4(swB + 4);
       dv[0] = mfma32(toB[1][0], pB1, dv[0]);  // d5
-#if !PICO_KVP_DMA_FRONT
+#if !PICO_KVP_DMA_FRONT && !PICO_KVP_STAGE
       if (dma_next) issue_piece(DSLOT, nxt, 2);
 #endif
       KVP_SLOT();
       dk[0] = mfma32(tqB[1][0], sB1, dk[0]);  // d6
-#if !PICO_KVP_DMA_FRONT
+#if !PICO_KVP_DMA_FRONT && !PICO_KVP_STAGE
       if (dma_next) issue_piece(DSLOT, nxt, 3);
 #endif
       KVP_SLOT();
       dv[1] = mfma32(toB[1][1], pB1, dv[1]);  // d7
-#if !PICO_KVP_DMA_FRONT
+#if !PICO_KVP_DMA_FRONT && !PICO_KVP_STAGE
       if (dma_next) issue_piece(DSLOT, nxt, 4);
 #endif
       KVP_SLOT();
       dk[1] = mfma32(tqB[1][1], sB1, dk[1]);  // d8
+#if PICO_KVP_STAGE
+      if (dma_next) stage_store(DSLOT);
+#endif
       advance(nxt);
       KVP_SLOT();
       KVP_ST(6);

@@ -46,14 +46,22 @@ __global__ __launch_bounds__(256) void rope_kernel(const bf16_t* __restrict__ x,
     const unsigned b = fdiv(r1, fs);
     const int s = (int)(r1 - b * fs.d);
     const int i = vi * 8;
+#ifndef PICO_ROPE_NT
+#define PICO_ROPE_NT 0
+#endif
     const u16x8 c = *reinterpret_cast<const u16x8*>(cosp + (int64_t)s * cs + i);
     const u16x8 sn = *reinterpret_cast<const u16x8*>(sinp + (int64_t)s * cs + i);
     u16x8 x1[HPT], x2[HPT];
 #pragma unroll
     for (int k = 0; k < HPT; ++k) {
       const bf16_t* xp = x + (int64_t)b * xs0 + (int64_t)s * xs1 + (int64_t)(hg * HPT + k) * xs2 + i;
+#if PICO_ROPE_NT  // streaming loads (A/B variant: the input is read once)
+      x1[k] = __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(xp));
+      x2[k] = __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(xp + half));
+#else
       x1[k] = *reinterpret_cast<const u16x8*>(xp);
       x2[k] = *reinterpret_cast<const u16x8*>(xp + half);
+#endif
     }
 #pragma unroll
     for (int k = 0; k < HPT; ++k) {
