@@ -1036,7 +1036,6 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kvp_kernel(const pico
   unsigned long long ph[16] = {0}, tlast = 0, tblk = 0;
   ph[10] = __builtin_amdgcn_s_memrealtime();
   ph[12] = __builtin_amdgcn_s_memtime();
-  tblk = ph[12];
 #define KVP_ST(i)                                          \
   {                                                        \
     const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
@@ -1065,32 +1064,24 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kvp_kernel(const pico
   const int nblk_wg = grp.n ? (int)((grp.cnt >> (4 * gi)) & 15u) : 1;
   const unsigned delta_off = (unsigned)((const char*)delta_g - (const char*)sinit_g);  // same workspace
   const unsigned ring_lds = (unsigned)__builtin_amdgcn_readfirstlane((int)lds_addr(smem));
-  const int lane = lane0, r = lane & 31, h = lane >> 5;
-
-  // The group's key blocks are ONE tile stream: the DMA cursor runs from one block's last tile into the next
-  // block's first (no ring drain), and the next block's K / V fragments are loaded during the current block's
-  // last tile, so a block switch costs its epilogue's stores and not a prologue (round 5: the per-block prologue
-  // was 17 % of a wave's lifetime at C2, profiles/r05_kvp_stamps_m2b_dma.json).
-  struct Blk {
-    int k0, qstart, qend, ntiles, hq0, q00;
-  };
-  auto blk = [&](int jb) __attribute__((always_inline)) {
-    Blk B;
-    const int kb = grp.n ? (int)((gw >> (8 * jb)) & 255u) : gi;
-    B.k0 = kb * KVB;
-    B.qstart = CAUSAL ? B.k0 : 0;  // k0 is a multiple of QT2
-    const int nqt = Sq > B.qstart ? (Sq - B.qstart + QT2 - 1) / QT2 : 0;
-    const int ntot = G * nqt;
-    const int tb = (int)((int64_t)ntot * hs / hsplit);
-    B.ntiles = (int)((int64_t)ntot * (hs + 1) / hsplit) - tb;
-    B.hq0 = hk * G + (nqt ? tb / nqt : 0);
-    B.q00 = B.qstart + (nqt ? tb % nqt : 0) * QT2;
-    B.qend = B.qstart + nqt * QT2;
-    return B;
-  };
-  int total = 0;
 #pragma clang loop unroll(disable)
-  for (int jb = 0; jb < nblk_wg; ++jb) total += blk(jb).ntiles;
+  for (int jb = 0; jb < nblk_wg; ++jb) {
+#if PICO_KVP_STAMP
+  tblk = __builtin_amdgcn_s_memtime();
+#endif
+  const int kb = grp.n ? (int)((gw >> (8 * jb)) & 255u) : gi;
+  if (jb > 0) lds_barrier();
+  int lane_l = lane0;
+  asm volatile("" : "+v"(lane_l));
+  const int lane = lane_l, r = lane & 31, h = lane >> 5;
+  const int k0 = kb * KVB;
+  const int kw = k0 + 32 * wave;
+  const int qstart = CAUSAL ? k0 : 0;  // k0 is a multiple of QT2
+  const int nqt = Sq > qstart ? (Sq - qstart + QT2 - 1) / QT2 : 0;
+  const int ntot = G * nqt;
+  const int tb = (int)((int64_t)ntot * hs / hsplit);
+  const int ntiles = (int)((int64_t)ntot * (hs + 1) / hsplit) - tb;
+  const int hq0 = hk * G + (nqt ? tb / nqt : 0), q00 = qstart + (nqt ? tb % nqt : 0) * QT2;
 
   // ---- tile DMA: this wave's pieces i = 0..3 are image pieces j = wave + 4 i (Q: j < 8, dO: 8 <= j < 16);
   // wave 0 also issues the LSE / delta piece (lanes 0-15: -LSE/scale rows 4l..4l+3, 16-31: -delta rows, 32-63
@@ -1098,49 +1089,38 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kvp_kernel(const pico
   const int64_t qs1 = a.q_strides[1] * 2, ds1 = a.do_strides[1] * 2;  // bytes per query row
   const char* const qbase = (const char*)((const bf16_t*)a.q + b * a.q_strides[0]);
   const char* const dobase = (const char*)((const bf16_t*)a.dout + b * a.do_strides[0]);
+  int pc_row[4];
   unsigned pc_off[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int jj = (wave + 4 * i) % C::NQP;
-    const int row = C::RPP * jj + lane / CPR;
-    pc_off[i] = (unsigned)(row * (i < 2 ? qs1 : ds1) + 8 * ((lane % CPR) ^ swz<64>(row)) * 2);
+    pc_row[i] = C::RPP * jj + lane / CPR;
+    pc_off[i] = (unsigned)(pc_row[i] * (i < 2 ? qs1 : ds1) + 8 * ((lane % CPR) ^ swz<64>(pc_row[i])) * 2);
   }
-  // the DMA cursor: tile (hq, q0) of block jb (rows [qs, qe) of each query head), `left` tiles of it to come
   struct Tc {
-    int hq, q0, qs, qe, jb, left;
+    int hq, q0;
     const char* qp;
     const char* dp;
     const char* lp;
   };
-  auto make_tc = [&](int hq, int q0, int qs, int qe, int jb, int left) __attribute__((always_inline)) {
+  auto make_tc = [&](int hq, int q0) __attribute__((always_inline)) {
     Tc c;
     c.hq = hq;
     c.q0 = q0;
-    c.qs = qs;
-    c.qe = qe;
-    c.jb = jb;
-    c.left = left;
     c.qp = qbase + hq * a.q_strides[2] * 2 + q0 * qs1;
     c.dp = dobase + hq * a.do_strides[2] * 2 + q0 * ds1;
     c.lp = (const char*)(sinit_g + ((int64_t)b * Hq + hq) * sq_pad + q0);
     return c;
   };
-  auto first_tc = [&](int jb) __attribute__((always_inline)) {
-    const Blk B = blk(jb);
-    return make_tc(B.hq0, B.q00, B.qstart, B.qend, jb, B.ntiles);
-  };
+  const int qend = qstart + nqt * QT2;
   auto advance = [&](Tc& c) __attribute__((always_inline)) {
-    if (c.left <= 1) {
-      if (c.jb + 1 < nblk_wg) c = first_tc(c.jb + 1);  // the stream continues into the next block
-      else c.left = 0;
-    } else if (c.q0 + QT2 >= c.qe) {
-      c = make_tc(c.hq + 1, c.qs, c.qs, c.qe, c.jb, c.left - 1);
+    if (c.q0 + QT2 >= qend) {
+      c = make_tc(c.hq + 1, qstart);
     } else {
       c.q0 += QT2;
       c.qp += QT2 * qs1;
       c.dp += QT2 * ds1;
       c.lp += QT2 * 4;
-      c.left -= 1;
     }
   };
   const bool ragged = Sq % QT2 != 0;
@@ -1169,10 +1149,10 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kvp_kernel(const pico
 #pragma unroll
     for (int i = 0; i < 5; ++i) issue_piece(si, c, i);
   };
-  Tc nxt = first_tc(0);
+  Tc nxt = make_tc(hq0, q00);
 #pragma unroll
   for (int j = 0; j < C::PD; ++j) {
-    if (j < total) issue(j, nxt);
+    if (j < ntiles) issue(j, nxt);
     advance(nxt);
   }
 
@@ -1180,8 +1160,8 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kvp_kernel(const pico
   const bf16_t* kg = (const bf16_t*)a.k + b * a.k_strides[0] + hk * a.k_strides[2];
   const bf16_t* vg = (const bf16_t*)a.v + b * a.v_strides[0] + hk * a.v_strides[2];
   bf16x8 kf[KS], vf[KS];
-  auto load_kv = [&](int kwn) __attribute__((always_inline)) {
-    const int key = kwn + r;
+  {
+    const int key = kw + r;
     const bool ok = key < Sk;
     const bf16_t* kp = kg + (int64_t)min(key, Sk - 1) * a.k_strides[1] + 8 * h;
     const bf16_t* vp = vg + (int64_t)min(key, Sk - 1) * a.v_strides[1] + 8 * h;
@@ -1192,11 +1172,9 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kvp_kernel(const pico
       kf[ks] = __builtin_bit_cast(bf16x8, ok ? kv : (u16x8)0);
       vf[ks] = __builtin_bit_cast(bf16x8, ok ? vv : (u16x8)0);
     }
-  };
-  Blk cb = blk(0);  // the consumer's block
-  int cjb = 0, cleft = cb.ntiles;
-  int kw = cb.k0 + 32 * wave;  // this wave's first key
-  load_kv(kw);
+  }
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) asm volatile("" : "+v"(kf[ks]), "+v"(vf[ks]));
   f32x16 dk[DT], dv[DT];
 #pragma unroll
   for (int dt = 0; dt < DT; ++dt) {
@@ -1211,6 +1189,8 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kvp_kernel(const pico
   for (int ks = 0; ks < KS; ++ks) asm volatile("" : "+v"(qo[ks]));
 #pragma unroll
   for (int dt = 0; dt < DT; ++dt) asm volatile("" : "+v"(tro[dt][0]), "+v"(tro[dt][1]));
+  const bool kpad = kw + 31 >= Sk;  // wave-uniform: some of the wave's keys are padding
+  const int mykey = kw + r;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
@@ -1227,87 +1207,37 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kvp_kernel(const pico
     return v;
   };
   // diagonal / padding-key mask on an S initial value: -inf where key > query row (causal) or key >= Sk
-  auto mask_rows = [&](f32x16& s, int qrow0, int mykey) __attribute__((always_inline)) {
+  auto mask_rows = [&](f32x16& s, int qrow0) __attribute__((always_inline)) {
     const int rel = mykey >= Sk ? 1 << 30 : (CAUSAL ? mykey - qrow0 - 4 * h : -1);
 #pragma unroll
     for (int i = 0; i < 16; ++i) s[i] = ((i & 3) + 8 * (i >> 2) < rel) ? -INFINITY : s[i];
   };
-  // ---- epilogue of the consumer's block: lane = key kw + r, register i of tile dt = d 32 dt + acc_row(i, h) ----
-  auto epilogue = [&]() __attribute__((always_inline)) {
-    if (hsplit == 1) {
-      const int key = kw + r;
-      const int kc = min(key, Sk - 1);
-      if (a.flags & PICO_ATTN_ROPE_BWD) {
-        const bf16_t* cp = (const bf16_t*)a.rope_cos + (int64_t)kc * a.rope_stride;
-        const bf16_t* sp = (const bf16_t*)a.rope_sin + (int64_t)kc * a.rope_stride;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const u16x4 c4 = *reinterpret_cast<const u16x4*>(cp + 8 * g + 4 * h);
-          const u16x4 s4 = *reinterpret_cast<const u16x4*>(sp + 8 * g + 4 * h);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const float cf = bf2f(c4[j]), sn = bf2f(s4[j]);
-            const float x1 = dk[0][4 * g + j], x2 = dk[1][4 * g + j];
-            dk[0][4 * g + j] = x1 * cf + x2 * sn;
-            dk[1][4 * g + j] = x2 * cf - x1 * sn;
-          }
-        }
-      }
-      bf16_t* dkp = (bf16_t*)a.dk + b * a.dk_strides[0] + hk * a.dk_strides[2] + (int64_t)kc * a.dk_strides[1];
-      bf16_t* dvp = (bf16_t*)a.dv + b * a.dv_strides[0] + hk * a.dv_strides[2] + (int64_t)kc * a.dv_strides[1];
-      store_row_bf16_x16<DT>(dkp, h, key < Sk, [&](int dt, int i) { return dk[dt][i] * scale; });
-      store_row_bf16_x16<DT>(dvp, h, key < Sk, [&](int dt, int i) { return dv[dt][i]; });
-    } else {  // fp32 partials [hs][dK | dV][b][key][hk][D]
-      const int64_t part = a.batch * a.seqlen_k * a.heads_kv * 64;
-      float* pk = dkv_part + (int64_t)(2 * hs) * part + ((int64_t)b * Sk * a.heads_kv + hk) * 64;
-      float* pv = pk + part;
-      const int key = kw + r;
-      if (key < Sk) {
-#pragma unroll
-        for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            f32x4 wk, wv;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              wk[j] = dk[dt][4 * g + j] * scale;
-              wv[j] = dv[dt][4 * g + j];
-            }
-            const int64_t o = (int64_t)key * a.heads_kv * 64 + 32 * dt + 8 * g + 4 * h;
-            *reinterpret_cast<f32x4*>(pk + o) = wk;
-            *reinterpret_cast<f32x4*>(pv + o) = wv;
-          }
-      }
-    }
-  };
 #if PICO_KVP_STAMP
-  ph[8] += __builtin_amdgcn_s_memtime() - tblk;  // prologue (first block)
+  ph[8] += __builtin_amdgcn_s_memtime() - tblk;  // prologue of this block
 #endif
-  int q0cur = cb.q00;
-  for (int t0 = 0; t0 < total; t0 += C::NBUF) {
+  int q0cur = q00;
+  for (int t0 = 0; t0 < ntiles; t0 += C::NBUF) {
 #pragma unroll
     for (int u = 0; u < C::NBUF; ++u) {
       const int t = t0 + u;
-      if (t >= total) break;
+      if (t >= ntiles) break;
 #if PICO_KVP_STAMP
       tlast = __builtin_amdgcn_s_memtime();
       ph[7] += 1;
 #endif
       if (t > 0) {
         // this wave's pieces of tile t landed; those of the younger tiles already issued stay in flight
-        const int younger = min(C::PD - 1, total - 1 - t);
+        const int younger = min(C::PD - 1, ntiles - 1 - t);
         wait_vmcnt(younger * (wave == 0 ? 5 : 4));
         KVP_ST(0);
         lds_barrier();  // every wave's pieces of tile t visible; the slot of tile t - 1 is no longer read
         KVP_ST(1);
       }
-      // the DMA of tile t + PD is issued in the gaps of this tile's last MFMA phase (M2(B)), one piece per slot
-      // (an LDS-DMA instruction stalls its wave ~90 cycles at issue; stamps)
-      const bool dma_next = t + C::PD < total;
+      // the DMA of tile t + PD is issued in the gaps of this tile's last MFMA phase (M2(B)), one piece per slot:
+      // an LDS-DMA instruction stalls its wave ~90 cycles at issue (stamps: 462 cycles per tile for the five
+      // pieces issued back to back after the barrier); behind an MFMA that stall runs under the matrix pipe
+      const bool dma_next = t + C::PD < ntiles;
       const int DSLOT = (u + C::PD) % C::NBUF;  // a constant after unrolling
-      const bool last_of_blk = cleft == 1;
-      const int mykey = kw + r;
-      const bool kpad = kw + 31 >= Sk;  // wave-uniform: some of the wave's keys are padding
       KVP_SLOT();
       KVP_ST(2);
       const char* qs = smem + u * C::SLOT;
@@ -1342,7 +1272,7 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kvp_kernel(const pico
       qa[1] = lds_read_b128(qs, qo[1]);
       f32x16 sA = init_rows(lsd, 0, 0);
       f32x16 dpA = init_rows(lsd, 0, 1);
-      if (diag) mask_rows(sA, q0cur, mykey);
+      if (diag) mask_rows(sA, q0cur);
       f32x16 sB, dpB;
       KVP_SLOT();
       sA = mfma32(qa[0], kf[0], sA);  // a1
@@ -1366,7 +1296,7 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kvp_kernel(const pico
       dpA = mfma32(da[1], vf[1], dpA);  // a6
       qb[0] = lds_read_b128(qs, qo[0] + 32 * RB);
       qb[1] = lds_read_b128(qs, qo[1] + 32 * RB);
-      if (diagB) mask_rows(sB, q0cur + 32, mykey);
+      if (diagB) mask_rows(sB, q0cur + 32);
       KVP_SLOT();
       dpA = mfma32(da[2], vf[2], dpA);  // a7
       qb[2] = lds_read_b128(qs, qo[2] + 32 * RB);
@@ -1409,9 +1339,6 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kvp_kernel(const pico
       toA[1][1] = tr_pair(dos + 16 * RB, tro[1][0], tro[1][1]);
       KVP_SLOT();
       KVP_ST(4);
-      // the next key block's K / V fragments (the group's blocks form one tile stream): requested right after this
-      // block's last M1, their latency runs under M2(A), M2(B) and this block's epilogue
-      if (last_of_blk && cjb + 1 < nblk_wg) load_kv(blk(cjb + 1).k0 + 32 * wave);
       const bf16x8 pA0 = pk4(pwA), sA0 = pk4(swA);
       dv[0] = mfma32(toA[0][0], pA0, dv[0]);  // c1
       vpair(sA, dpA, 6, pwA[6], swA[6]);
@@ -1472,41 +1399,68 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kvp_kernel(const pico
       if (dma_next) issue_piece(DSLOT, nxt, 4);
       KVP_SLOT();
       dk[1] = mfma32(tqB[1][1], sB1, dk[1]);  // d8
-      KVP_SLOT();
       advance(nxt);
       KVP_SLOT();
       KVP_ST(6);
-      if (last_of_blk) {
-#if PICO_KVP_STAMP
-        tblk = __builtin_amdgcn_s_memtime();
-#endif
-        epilogue();
-#pragma unroll
-        for (int dt = 0; dt < DT; ++dt) {
-          dk[dt] = (f32x16)0.f;
-          dv[dt] = (f32x16)0.f;
-        }
-        if (cjb + 1 < nblk_wg) {
-          cjb += 1;
-          cb = blk(cjb);
-          cleft = cb.ntiles;
-          kw = cb.k0 + 32 * wave;
-          q0cur = cb.q00;
-        } else {
-          cleft = 0;
-        }
-#if PICO_KVP_STAMP
-        ph[9] += __builtin_amdgcn_s_memtime() - tblk;
-#endif
-      } else {
-        cleft -= 1;
-        q0cur = q0cur + QT2 >= cb.qend ? cb.qstart : q0cur + QT2;
-      }
+      q0cur = q0cur + QT2 >= qend ? qstart : q0cur + QT2;
     }
   }
-  if (total == 0) epilogue();  // a block no query row sees: dK = dV = 0
+#if PICO_KVP_STAMP
+  tblk = __builtin_amdgcn_s_memtime();
+#endif
+
+  // ---- epilogue (as attn_bwd_kv_kernel): lane = key kw + r, register i of tile dt = d 32 dt + acc_row(i, h) ----
+  if (hsplit == 1) {
+    const int key = kw + r;
+    const int kc = min(key, Sk - 1);
+    if (a.flags & PICO_ATTN_ROPE_BWD) {
+      const bf16_t* cp = (const bf16_t*)a.rope_cos + (int64_t)kc * a.rope_stride;
+      const bf16_t* sp = (const bf16_t*)a.rope_sin + (int64_t)kc * a.rope_stride;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const u16x4 c4 = *reinterpret_cast<const u16x4*>(cp + 8 * g + 4 * h);
+        const u16x4 s4 = *reinterpret_cast<const u16x4*>(sp + 8 * g + 4 * h);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float cf = bf2f(c4[j]), sn = bf2f(s4[j]);
+          const float x1 = dk[0][4 * g + j], x2 = dk[1][4 * g + j];
+          dk[0][4 * g + j] = x1 * cf + x2 * sn;
+          dk[1][4 * g + j] = x2 * cf - x1 * sn;
+        }
+      }
+    }
+    bf16_t* dkp = (bf16_t*)a.dk + b * a.dk_strides[0] + hk * a.dk_strides[2] + (int64_t)kc * a.dk_strides[1];
+    bf16_t* dvp = (bf16_t*)a.dv + b * a.dv_strides[0] + hk * a.dv_strides[2] + (int64_t)kc * a.dv_strides[1];
+    store_row_bf16_x16<DT>(dkp, h, key < Sk, [&](int dt, int i) { return dk[dt][i] * scale; });
+    store_row_bf16_x16<DT>(dvp, h, key < Sk, [&](int dt, int i) { return dv[dt][i]; });
+  } else {  // fp32 partials [hs][dK | dV][b][key][hk][D]
+    const int64_t part = a.batch * a.seqlen_k * a.heads_kv * 64;
+    float* pk = dkv_part + (int64_t)(2 * hs) * part + ((int64_t)b * Sk * a.heads_kv + hk) * 64;
+    float* pv = pk + part;
+    const int key = kw + r;
+    if (key < Sk) {
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          f32x4 wk, wv;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            wk[j] = dk[dt][4 * g + j] * scale;
+            wv[j] = dv[dt][4 * g + j];
+          }
+          const int64_t o = (int64_t)key * a.heads_kv * 64 + 32 * dt + 8 * g + 4 * h;
+          *reinterpret_cast<f32x4*>(pk + o) = wk;
+          *reinterpret_cast<f32x4*>(pv + o) = wv;
+        }
+    }
+  }
 #if PICO_KVP_STAMP
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  ph[9] += __builtin_amdgcn_s_memtime() - tblk;  // epilogue of this block (stores drained)
+#endif
+  }  // key blocks of the group
+#if PICO_KVP_STAMP
   ph[11] = __builtin_amdgcn_s_memrealtime();
   ph[13] = __builtin_amdgcn_s_memtime();
   if ((threadIdx.x & 63) == 0 && blockIdx.x < 8192) {
@@ -1523,9 +1477,15 @@ bool qp_enabled() {
   return e && e[0] == '1';
 }
 
-bool kvp_enabled() {
+// attn_bwd_kvp_kernel (64-row tiles, two workgroups per CU) for D = 64 up to 2048 keys, the 32-row kernel beyond:
+// same box, 3 interleaved rounds (profiles/r05_ab_kvp_default.jsonl): dK/dV C2 55.2 -> 53.5 us, GQA-4 57.4 -> 53.2,
+// C2 non-causal 76.7 -> 72.7, but S 4096 138.8 -> 147.2. PICO_ATTN_KVP=0 / 1 forces it off / on (A/B switch).
+bool kvp_enabled(const pico_attn_args* a) {
+  if (a->head_dim != 64) return false;
   const char* e = getenv("PICO_ATTN_KVP");
-  return e && e[0] == '1';
+  if (e && e[0] == '0') return false;
+  if (e && e[0] == '1') return true;
+  return a->seqlen_k <= 2048;
 }
 #endif  // !PICO_SPLIT_D128_TU
 
@@ -1545,7 +1505,7 @@ int64_t split_lsd_floats(const pico_attn_args* a) {
 int kv_minb(const pico_attn_args* a) {
   if (a->head_dim == 128) return 1;
 #ifndef PICO_SPLIT_D128_TU
-  if (kvp_enabled()) return 2;  // attn_bwd_kvp_kernel: two waves per SIMD, <= 256 VGPRs
+  if (kvp_enabled(a)) return 2;  // attn_bwd_kvp_kernel: two waves per SIMD, <= 256 VGPRs
 #endif
   return a->causal ? 3 : 2;
 }
@@ -1631,9 +1591,7 @@ BlkGroups block_groups(const int* wt, int nblk, int64_t nbh, int minb) {
 
 // dK/dV kernel groups: key block kb sees (Hq / Hkv) * ceil((Sq - 128 kb) / 32) query tiles (causal, no hsplit)
 BlkGroups kv_groups(const pico_attn_args* a, int hsplit, int minb) {
-  // (causal self-attention only: every key block then has query tiles, which attn_bwd_kvp_kernel's one tile stream
-  // per group assumes)
-  if (!a->causal || hsplit != 1 || a->heads_kv <= 0 || a->seqlen_q != a->seqlen_k) return BlkGroups{};
+  if (!a->causal || hsplit != 1 || a->heads_kv <= 0) return BlkGroups{};
   const int nkb = (int)((a->seqlen_k + KVB - 1) / KVB);
   if (nkb > 32) return BlkGroups{};
   int wt[32];
@@ -1652,7 +1610,7 @@ int launch_split(const pico_attn_args* a, hipStream_t s) {
   float* dkv_part = delta + split_lsd_floats(a);
   const float sl2 = a->softmax_scale * LOG2E;
 #ifndef PICO_SPLIT_D128_TU
-  const bool use_kvp = D == 64 && kvp_enabled();
+  const bool use_kvp = D == 64 && kvp_enabled(a);
 #else
   constexpr bool use_kvp = false;
 #endif

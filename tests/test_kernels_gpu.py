@@ -415,6 +415,64 @@ def test_attention_bwd_d128_key_block_groups(S, Hq, Hkv, causal, mode):
     assert rel_l2(dv.float(), gv) < 1e-2
 
 
+@pytest.mark.parametrize("B,Sq,Sk,Hq,Hkv,causal,mode", [
+    (2, 1024, 1024, 8, 8, True, "bf16"),     # C2 slice, block groups
+    (1, 1000, 1000, 8, 2, True, "bf16"),     # ragged, GQA 4
+    (4, 1024, 1024, 32, 8, True, "bf16"),    # GQA 4 at a small grid: key blocks split over workgroups (hsplit)
+    (1, 2048, 2048, 4, 4, True, "rope"),     # the default's last length, fused RoPE^-1
+    (1, 2049, 2049, 2, 2, True, "f32acc"),   # past it (default: the 32-row kernel), caller's fp32 dQ
+    (2, 96, 200, 4, 4, False, "bf16"),       # cross lengths, non-causal
+    (1, 640, 640, 4, 4, False, "rope"),
+])
+def test_attention_bwd_d64_kv_kernels(monkeypatch, B, Sq, Sk, Hq, Hkv, causal, mode):
+    """D = 64 dK/dV: attn_bwd_kvp_kernel (64-row query tiles; the default up to 2048 keys) and the 32-row
+    attn_bwd_kv_kernel (PICO_ATTN_KVP=0 / 1 force either), each with its matching dQ-kernel LSE form, vs an fp32 torch
+    reference, and the two within bf16 rounding of each other."""
+    from picotron_amd.model import get_cos_sin
+    ops = _ops()
+    torch.manual_seed(Sq * 3 + Sk + Hq + Hkv)
+    D = 64
+    q, do = [torch.randn(B, Sq, Hq, D, dtype=BF, device=DEV) for _ in range(2)]
+    k, v = [torch.randn(B, Sk, Hkv, D, dtype=BF, device=DEV) for _ in range(2)]
+    sc = 1.0 / math.sqrt(D)
+    o, lse = ops.attention_block_fwd(q, k, v, sc, causal)
+    G = Hq // Hkv
+    qf, kf, vf = [t.float().transpose(1, 2).requires_grad_(True) for t in (q, k, v)]
+    kr, vr = kf.repeat_interleave(G, 1), vf.repeat_interleave(G, 1)
+    sm = (qf @ kr.transpose(-1, -2)) * sc
+    if causal:
+        sm = sm.masked_fill(torch.triu(torch.ones(Sq, Sk, dtype=torch.bool, device=DEV), 1 + Sk - Sq), float("-inf"))
+    out = torch.softmax(sm, -1) @ vr
+    gq, gk, gv = torch.autograd.grad(out, (qf, kf, vf), do.float().transpose(1, 2))
+    gq, gk, gv = (t.transpose(1, 2) for t in (gq, gk, gv))
+    cos = sin = None
+    if mode == "rope":
+        cos, sin = get_cos_sin(max(Sq, Sk), D, base=10000.0)
+        cos, sin = cos.to(DEV, BF)[:, : D // 2], sin.to(DEV, BF)[:, : D // 2]
+        rq, rk = torch.empty_like(q), torch.empty_like(k)
+        ops._rope_launch(gq.to(BF).contiguous(), rq, cos, sin, True)
+        ops._rope_launch(gk.to(BF).contiguous(), rk, cos, sin, True)
+        gq, gk = rq.float(), rk.float()
+    res = {}
+    for kvp in ("0", "1"):
+        monkeypatch.setenv("PICO_ATTN_KVP", kvp)
+        if mode == "bf16":
+            dq, dk, dv = ops.attention_block_bwd(do, q, k, v, o, lse, sc, causal)
+        elif mode == "f32acc":
+            dq = torch.full(q.shape, 0.25, dtype=torch.float32, device=DEV)
+            _, dk, dv = ops.attention_block_bwd(do, q, k, v, o, lse, sc, causal, dq_accum=dq)
+            dq = dq - 0.25
+        else:
+            dq, dk, dv = [torch.empty_like(t) for t in (q, k, v)]
+            ops._attention_bwd_into(do, q, k, v, o, lse, sc, causal, dq, dk, dv, rope=(cos, sin))
+        torch.cuda.synchronize()
+        res[kvp] = [t.float() for t in (dq, dk, dv)]
+        for a, b in zip(res[kvp], (gq, gk, gv)):
+            assert rel_l2(a, b) < 1e-2, (kvp, rel_l2(a, b))
+    for a, b in zip(res["0"], res["1"]):
+        assert rel_l2(a, b) < 8e-3
+
+
 def test_attention_dq_f32_accumulate():
     ops = _ops()
     torch.manual_seed(3)
