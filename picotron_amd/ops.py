@@ -173,6 +173,12 @@ def _norm_grad_target(p, w):
         if mg is not None and getattr(p, "_pico_wgrad_ready", None) is not None:
             if mg.dtype == torch.float32 and mg.is_contiguous() and mg.shape == p.shape:
                 sync, world = p._pico_wgrad_sync()
+                if not sync and _norm_chain_enabled():
+                    # a non-syncing micro-batch: nothing waits for this bucket, so the dw reduction may be chained
+                    # into the next norm backward (its readiness call only records the parameter as produced by a
+                    # fused path, which must happen now, before its AccumulateGrad hook runs)
+                    p._pico_wgrad_ready()
+                    return 2, mg, 1.0, None
                 return 2, mg, (1.0 / world if sync else 1.0), p._pico_wgrad_ready
         elif mg is None and not _has_hooks(p):
             g = p.grad
@@ -363,6 +369,14 @@ def wgrad_fusion_enabled():
     return os.getenv("PICO_WGRAD_FUSION", "1") != "0"
 
 
+def _dp_stacked_mode():
+    """PICO_DP_STACKED: how the row-stacked parameters' (q|k|v, gate|up) weight gradients reach their fp32
+    main_grads under DataParallelBucket — "gemm" (one fp32-output GEMM per parameter into its main_grad) or
+    "accum" (one bf16 GEMM over the stack, then pico_grad_accum per parameter: the reference's bf16 dW + hook
+    sequence)."""
+    return os.getenv("PICO_DP_STACKED", "gemm")
+
+
 def wgrad_accumulate(params, dy2, x2):
     """dW = dy2^T x2 for row-stacked `params` ([sum rows, K]); returns the grads for autograd
     (None where the GEMM already accumulated into the parameter's gradient storage)."""
@@ -389,6 +403,20 @@ def wgrad_accumulate(params, dy2, x2):
         # the forward that first uses the parameter, so in the two-stream pipelined graph (forward i + 1 beside
         # backward i) the node of micro-batch i served micro-batch i + 1 too, and torch synchronised the two
         # streams on every such gradient ("AccumulateGrad node's stream does not match ...").
+        if _dp_stacked_mode() == "gemm":
+            # one fp32-output GEMM per parameter on its rows of dy (a column slice of dy2: no copy), accumulating
+            # into main_grad in the GEMM's epilogue as the single-parameter branch above does — no bf16 dW
+            # buffer and no separate accumulate pass over main_grad
+            r0 = 0
+            for p in params:
+                n = p.shape[0]
+                sync, world = p._pico_wgrad_sync()
+                sc = 1.0 / world if sync else 1.0
+                torch.addmm(p.main_grad, dy2[:, r0:r0 + n].t(), x2, beta=sc, alpha=sc, out_dtype=torch.float32,
+                            out=p.main_grad)
+                p._pico_wgrad_ready()
+                r0 += n
+            return (None,) * len(params)
         from .data_parallel.bucket import get_kernels
         buf = torch.mm(dy2.t(), x2)
         r0 = 0
