@@ -356,7 +356,7 @@ def main():
                        "schedule": ("eager" if not args.graphs else
                                     "pipelined graph (forward i beside backward i-1)" if pipelined_enabled() else
                                     "graph per micro-batch"),
-                       "wgrad": ("paired micro-batches (one GEMM per projection per two micro-batches)"
+                       "wgrad": ("grouped micro-batches (one GEMM per projection per %d micro-batches)" % _WP.group_size()
                                  if _WP.enabled() and (not args.graphs or pipelined_enabled()) else "per micro-batch")},
             "tokens_per_sec_per_gpu": round(tps_gpu, 1),
             "mfu_pct": round(mfu, 2),

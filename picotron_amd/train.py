@@ -223,6 +223,7 @@ class PipelinedMicroBatchGraph:
     def _body(self, inp, tgt):
         from . import ops
         model, n, acc = self.model, self.n, self.loss_acc
+        WP.begin_step()  # each run of the body (eager warm-up, capture) issues the step's micro-batches from 0
         cur = torch.cuda.current_stream()
         # no dgrad / wgrad side-stream pairs (ops.dgrad_wgrad) inside the pipeline: a fork from slot 1's stream
         # crashes the capture (ops.no_side_streams), and on slot 0 alone they measured slower (C2 154.2 -> 152.2 K
@@ -232,6 +233,19 @@ class PipelinedMicroBatchGraph:
         # segfaults on this ROCm (scripts/dbg_event_capture.py reproduces it with plain tensor ops)
         streams = (cur, self.streams[1])
         streams[1].wait_stream(cur)
+        # the paired weight-gradient GEMMs on a third stream (ops.wgrad_stream), joined at the end: off the
+        # backward chain, beside its HBM-bound kernels and the other slot's work
+        wst = self.streams[2] if ops.wgrad_stream_enabled() and WP.enabled() else None
+        if wst is not None:
+            wst.wait_stream(cur)
+        with (ops.wgrad_stream(wst, cur) if wst is not None else contextlib.nullcontext()):
+            self._slots(model, n, acc, streams, inp, tgt)
+        cur.wait_stream(streams[1])
+        if wst is not None:
+            cur.wait_stream(wst)
+
+    def _slots(self, model, n, acc, streams, inp, tgt):
+        from . import ops
         k = inp.shape[0]
         losses = [None] * k
         bwd_done = fwd_done = None
@@ -256,12 +270,12 @@ class PipelinedMicroBatchGraph:
                     losses[i] = _forward_loss(model, inp[i], tgt[i], n, acc)
                     fwd_done = torch.cuda.Event()
                     fwd_done.record(st)
-        cur.wait_stream(streams[1])
 
     def _capture(self, batches):
         dev = batches[0][0].device
         if self.streams is None:
-            self.streams = (None, torch.cuda.Stream(device=dev))  # slot 0: the caller's (capture) stream
+            # slot 0: the caller's (capture) stream; slot 1; the weight-gradient stream
+            self.streams = (None, torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev))
         inp = torch.stack([b[0] for b in batches])
         tgt = torch.stack([b[1] for b in batches])
         if self.loss_acc is None:

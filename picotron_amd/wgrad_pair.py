@@ -18,6 +18,10 @@ with no copy: the operands are already adjacent. dW is the same sum, accumulated
 (the pairing is verified per GEMM by pointer, never assumed); a second half whose own operands are elsewhere while
 its first half is pending copies them in and runs the pair GEMM.
 
+PICO_WGRAD_GROUP = G > 2 generalises the pairs to groups of G micro-batches (slot i % G, x^T set (i // G) % 2):
+the first G - 1 defer and the last runs one GEMM over K = G T tokens — and, under DataParallelBucket, one fp32
+read-modify-write of main_grad per G micro-batches instead of per two.
+
 Active only inside train.train_step / PipelinedMicroBatchGraph, which announce each micro-batch
 (`micro_batch(i, n)`), and with PICO_WGRAD_PAIR != 0. Not under MicroBatchGraph: its one captured micro-batch
 is replayed for every index.
@@ -45,6 +49,16 @@ def _put(weight, b):
 
 def enabled():
     return os.getenv("PICO_WGRAD_PAIR", "1") != "0"
+
+
+def group_size():
+    """PICO_WGRAD_GROUP: micro-batches per weight-gradient GEMM (2 = pairs; 4, the default: one GEMM over four,
+    K = 4T). C2 step, same box, 3 alternating rounds (profiles/r05_ab_wgrad_group.jsonl): 4 vs 2 — 823.7 -> 818.9 ms,
+    under DataParallelBucket 854.3 -> 837.3 ms (half the fp32 main_grad read-modify-writes)."""
+    g = int(os.getenv("PICO_WGRAD_GROUP", "4"))
+    if g < 2 or g > 8:
+        raise ValueError(f"PICO_WGRAD_GROUP={g}: 2..8 micro-batches per weight-gradient GEMM")
+    return g
 
 
 @contextlib.contextmanager
@@ -80,33 +94,83 @@ def restore_pending(state):
 
 
 class PairBuf:
-    """The pair buffers of one projection (weight [N, K]) for T tokens per micro-batch."""
+    """The group buffers of one projection (weight [N, K]) for T tokens per micro-batch and G micro-batches per
+    GEMM (G = 2: the pairs)."""
 
-    def __init__(self, N, K, T, dtype, device):
-        self.N, self.K, self.T = N, K, T
-        self.xt = [torch.empty((K, 2 * T), dtype=dtype, device=device) for _ in range(2)]
-        self.dy = torch.empty((2 * T, N), dtype=dtype, device=device)
-        self.pending = None  # the x^T set of a first half whose GEMM was deferred to the second
+    def __init__(self, N, K, T, dtype, device, G=2):
+        self.N, self.K, self.T, self.G = N, K, T, G
+        self.xt = [torch.empty((K, G * T), dtype=dtype, device=device) for _ in range(2)]
+        self.dy = torch.empty((G * T, N), dtype=dtype, device=device)
+        # (x^T set, next slot) of a group whose first members deferred their GEMM to its last member, or None
+        self.pending = None
+        # events recorded after the last weight-gradient GEMM that read these buffers on another stream (the
+        # pipelined graph's wgrad stream): a producer on the capture stream waits for them before overwriting
+        self.xt_reader = [None, None]
+        self.dy_reader = None
 
     def xt_slot(self, i):
-        """Micro-batch i's x^T: [K, T] view, row stride 2T, in set (i // 2) % 2, columns of half i % 2."""
-        h = i % 2
-        return self.xt[(i // 2) % 2][:, h * self.T:(h + 1) * self.T]
+        """Micro-batch i's x^T: [K, T] view, row stride G T, in set (i // G) % 2, columns of slot i % G."""
+        h = i % self.G
+        return self.xt[(i // self.G) % 2][:, h * self.T:(h + 1) * self.T]
 
     def dy_slot(self, i):
-        h = i % 2
+        h = i % self.G
         return self.dy[h * self.T:(h + 1) * self.T]
+
+
+# (stream, origin stream) while the pipelined graph issues its weight-gradient GEMMs on a stream of their own
+_READERS = {"origin": None}
+
+
+@contextlib.contextmanager
+def reader_stream(origin):
+    """Within: the wgrad GEMMs may read the pair buffers on another stream (note_reader); producers on `origin`
+    (the capture stream) wait for the last such read of the half they overwrite. Producers on the other pipeline
+    slot do not wait: each follows a producer of the same buffer on `origin` through the slots' event chain (a
+    direct wait would put dependencies both ways between two forked capture streams, which this ROCm's
+    hipStreamEndCapture does not survive). Reader events never outlive the context."""
+    _clear_readers()
+    prev = _READERS["origin"]
+    _READERS["origin"] = origin
+    try:
+        yield
+    finally:
+        _READERS["origin"] = prev
+        _clear_readers()
+
+
+def _clear_readers():
+    for _, b in list(_BUFS.values()):
+        b.xt_reader = [None, None]
+        b.dy_reader = None
+
+
+def note_reader(weight, i, event):
+    """The wgrad GEMM of `weight` issued for micro-batch i read its pair buffers (dy, and x^T set (i // 2) % 2) on
+    another stream, done at `event`."""
+    b = _get(weight)
+    if b is None or _READERS["origin"] is None:
+        return
+    b.xt_reader[(i // b.G) % 2] = event
+    b.dy_reader = event
+
+
+def _wait_reader(ev):
+    o = _READERS["origin"]
+    if ev is not None and o is not None and torch.cuda.current_stream(o.device) == o:
+        o.wait_event(ev)
 
 
 def buf(weight, N, K, T, dtype, device):
     """The pair buffers of `weight` (created on first use; recreated if the shape changed)."""
     b = _get(weight)
-    if b is None or (b.N, b.K, b.T) != (N, K, T) or b.dy.dtype != dtype or b.dy.device != device:
+    G = group_size()
+    if b is None or (b.N, b.K, b.T, b.G) != (N, K, T, G) or b.dy.dtype != dtype or b.dy.device != device:
         if b is not None and b.pending is not None:
             raise RuntimeError("paired weight gradients (wgrad_pair) need the micro-batches of a pair to have one "
                                "shape; a first half is pending in buffers of another shape (PICO_WGRAD_PAIR=0 "
                                "turns the pairing off)")
-        b = PairBuf(N, K, T, dtype, device)
+        b = PairBuf(N, K, T, dtype, device, G)
         _put(weight, b)
     return b
 
@@ -116,7 +180,9 @@ def xt_out(weight, N, K, T, dtype, device):
     stride 2T), or None when pairing is off."""
     if not active() or weight is None:
         return None
-    return buf(weight, N, K, T, dtype, device).xt_slot(_CTX["i"])
+    b = buf(weight, N, K, T, dtype, device)
+    _wait_reader(b.xt_reader[(_CTX["i"] // b.G) % 2])
+    return b.xt_slot(_CTX["i"])
 
 
 def dy_out(weight, N, K, T, dtype, device):
@@ -124,7 +190,9 @@ def dy_out(weight, N, K, T, dtype, device):
     contiguous), or None when pairing is off."""
     if not active() or weight is None:
         return None
-    return buf(weight, N, K, T, dtype, device).dy_slot(_CTX["i"])
+    b = buf(weight, N, K, T, dtype, device)
+    _wait_reader(b.dy_reader)
+    return b.dy_slot(_CTX["i"])
 
 
 def dy_out_existing(weight, N, K, T, dtype, device):
@@ -135,12 +203,14 @@ def dy_out_existing(weight, N, K, T, dtype, device):
     b = _get(weight)
     if b is None or (b.N, b.K, b.T) != (N, K, T) or b.dy.dtype != dtype or b.dy.device != device:
         return None
+    _wait_reader(b.dy_reader)
     return b.dy_slot(_CTX["i"])
 
 
 def footprint_bytes():
-    """Bytes held by every live pair buffer: per projection (weight [N, K], T tokens per micro-batch) two x^T sets
-    [K, 2T] and one dy [2T, N] — (4 K T + 2 T N) elements; SmolLM-1.7B at T = 4096: about 0.9 GB per layer."""
+    """Bytes held by every live pair buffer: per projection (weight [N, K], T tokens per micro-batch, G per group)
+    two x^T sets [K, G T] and one dy [G T, N] — G (2 K T + T N) elements; SmolLM-1.7B at T = 4096, G = 2: about
+    0.9 GB per layer."""
     return sum(sum(x.numel() * x.element_size() for x in b.xt) + b.dy.numel() * b.dy.element_size()
                for _, b in list(_BUFS.values()))
 
@@ -161,34 +231,45 @@ def dy_out_if_paired(weight, x2, N, K, T, dtype, device):
     b = _get(weight)
     if b is None or (b.N, b.K, b.T) != (N, K, T) or x2.data_ptr() != b.xt_slot(_CTX["i"]).data_ptr():
         return None
+    _wait_reader(b.dy_reader)
     return b.dy_slot(_CTX["i"])
 
 
 def plan(weight, dy2, x2):
-    """How the wgrad of `weight` runs for the current micro-batch: ('skip',) — first half, deferred; or
-    ('gemm', dy, x) — one GEMM over (dy, x): the pair, or this micro-batch alone. A second half whose own operands
-    are not in the pair buffers while its first half is pending copies them there (a fallback: the producers
-    normally write them in place)."""
+    """How the wgrad of `weight` runs for the current micro-batch i: ('skip',) — deferred to the last member of
+    its group (micro-batches g0 .. g0 + r - 1, g0 = i - i % G, r = min(G, n - g0)); or ('gemm', dy, x) — one GEMM
+    over (dy, x): the group's first r slots, or this micro-batch alone. A member that continues a pending group
+    while its own operands are not in its slot copies them there (a fallback: the producers normally write them in
+    place); a member with no pending group before it runs its own GEMM."""
     b = _get(weight) if active() else None
     if b is None:
         return ("gemm", dy2, x2)
     i, n = _CTX["i"], _CTX["n"]
-    T = b.T
-    h = i % 2
+    T, G = b.T, b.G
+    h = i % G
+    s = (i // G) % 2
+    r = min(G, n - (i - h))
     mine = (dy2.data_ptr() == b.dy_slot(i).data_ptr() and tuple(dy2.shape) == (T, b.N)
-            and x2.data_ptr() == b.xt_slot(i).data_ptr() and tuple(x2.shape) == (T, b.K) and x2.stride() == (1, 2 * T))
-    if h == 0:
-        if mine and i + 1 < n:
-            b.pending = (i // 2) % 2
-            STATS["deferred"] += 1
-            return ("skip",)
-        return ("gemm", dy2, x2)
-    s = (i // 2) % 2
-    if b.pending is not None and b.pending == s:
-        b.pending = None
+            and x2.data_ptr() == b.xt_slot(i).data_ptr() and tuple(x2.shape) == (T, b.K) and x2.stride() == (1, G * T))
+    if b.pending is not None and b.pending != (s, h):
+        raise RuntimeError(f"wgrad_pair: micro-batch {i} of {n} reached a projection whose group state is "
+                           f"{b.pending} (x^T set, next slot): the deferred weight gradients of that group would be "
+                           "lost; the micro-batches of a step must be issued in order (begin_step() drops a group a "
+                           "failed step left)")
+    if h > 0 and b.pending == (s, h):
         if not mine:
+            _wait_reader(b.dy_reader)
             b.dy_slot(i).copy_(dy2)
             b.xt_slot(i).copy_(x2.t())
+        if h < r - 1:
+            b.pending = (s, h + 1)
+            STATS["deferred"] += 1
+            return ("skip",)
+        b.pending = None
         STATS["paired"] += 1
-        return ("gemm", b.dy, b.xt[s].t())
+        return ("gemm", b.dy[:r * T], b.xt[s][:, :r * T].t())
+    if h == 0 and mine and r > 1:
+        b.pending = (s, 1)
+        STATS["deferred"] += 1
+        return ("skip",)
     return ("gemm", dy2, x2)

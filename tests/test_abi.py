@@ -237,12 +237,13 @@ def test_train_step_groups_non_syncing_micro_batches():
     assert m.log == [("group", False, firsts[:3]), ("eager", True, firsts[3])], m.log
 
 
-def test_wgrad_pair_plan():
+def test_wgrad_pair_plan(monkeypatch):
     """wgrad_pair's decisions (host logic, CPU tensors): the first micro-batch of a pair whose operands sit in the
     pair buffers defers, the second runs one GEMM over both halves; no partner (odd grad_acc) or operands elsewhere
     -> its own GEMM; a second half not in place while its first half is pending is copied in; pairing off outside
     an announced micro-batch; a shape change with a first half pending raises."""
     from picotron_amd import wgrad_pair as WP
+    monkeypatch.setenv("PICO_WGRAD_GROUP", "2")
     w = torch.nn.Parameter(torch.zeros(6, 4))
     N, K, T = 6, 4, 8
 
@@ -290,6 +291,57 @@ def test_wgrad_pair_plan():
         import pytest
         with pytest.raises(RuntimeError, match="one shape"):
             WP.dy_out(w, N, K, 2 * T, torch.float32, torch.device("cpu"))
+    WP.begin_step()
+
+
+def test_wgrad_group_plan(monkeypatch):
+    """Groups of four (PICO_WGRAD_GROUP=4, the default): micro-batches 0-2 of a group defer, the fourth runs one
+    GEMM over the four slots (K = 4T, slot order = micro-batch order); a last partial group of r runs over its r
+    slots (r = 1: its own GEMM); x^T sets alternate per group; a group left pending when a new one starts raises
+    (its deferred weight gradients would be lost)."""
+    import pytest
+    from picotron_amd import wgrad_pair as WP
+    monkeypatch.setenv("PICO_WGRAD_GROUP", "4")
+    w = torch.nn.Parameter(torch.zeros(6, 4))
+    N, K, T = 6, 4, 8
+    cpu = torch.device("cpu")
+
+    def operands(i):
+        dy = WP.dy_out(w, N, K, T, torch.float32, cpu)
+        xt = WP.xt_out(w, N, K, T, torch.float32, cpu)
+        dy.copy_(torch.full_like(dy, float(i + 1)))
+        xt.copy_(torch.full_like(xt, float(10 * (i + 1))))
+        return dy, xt.t()
+
+    for n, tail in ((5, 1), (6, 2)):
+        WP.begin_step()
+        for i in range(n):
+            with WP.micro_batch(i, n):
+                dy, x = operands(i)
+                res = WP.plan(w, dy, x)
+                if i in (3, n - 1) and not (i == n - 1 and tail == 1):
+                    r = 4 if i == 3 else tail
+                    assert res[0] == "gemm" and res[1].shape == (r * T, N) and res[2].shape == (r * T, K), (n, i)
+                    g0 = i - (r - 1)
+                    for j in range(r):
+                        assert torch.equal(res[1][j * T:(j + 1) * T], torch.full((T, N), float(g0 + j + 1)))
+                        assert torch.equal(res[2][j * T:(j + 1) * T], torch.full((T, K), float(10 * (g0 + j + 1))))
+                    assert res[2].stride() == (1, 4 * T)
+                elif i == n - 1:  # a group of one: its own operands
+                    assert res[0] == "gemm" and res[1].data_ptr() == dy.data_ptr()
+                else:
+                    assert res == ("skip",), (n, i)
+        assert not WP.pending_state()
+    b = WP._get(w)
+    assert b.xt_slot(0).data_ptr() != b.xt_slot(4).data_ptr()  # groups 0 and 1 in different x^T sets
+    assert b.xt_slot(0).data_ptr() == b.xt_slot(8).data_ptr()
+    WP.begin_step()
+    with WP.micro_batch(0, 8):
+        dy, x = operands(0)
+        assert WP.plan(w, dy, x) == ("skip",)
+    with WP.micro_batch(0, 8), pytest.raises(RuntimeError, match=r"would be\s+lost"):
+        dy, x = operands(0)
+        WP.plan(w, dy, x)
     WP.begin_step()
 
 

@@ -270,15 +270,18 @@ _PAIR_CFG = dict(hidden_size=1024, intermediate_size=2048, num_attention_heads=1
                  num_hidden_layers=2, vocab_size=512, max_position_embeddings=128)
 
 
-@pytest.mark.parametrize("n,dp,graph", [(4, False, False), (3, False, False), (4, True, False), (4, False, True),
-                                        (3, True, True), (4, True, True)])
-def test_wgrad_pairs_match_unpaired(monkeypatch, n, dp, graph):
+@pytest.mark.parametrize("n,dp,graph,group", [(4, False, False, 2), (3, False, False, 2), (4, True, False, 2),
+                                              (4, False, True, 2), (3, True, True, 2), (4, True, True, 2),
+                                              (4, False, False, 4), (6, False, True, 4), (5, True, True, 4),
+                                              (8, True, True, 4)])
+def test_wgrad_pairs_match_unpaired(monkeypatch, n, dp, graph, group):
     """Paired weight gradients (wgrad_pair: two micro-batches' wgrad GEMMs as one over both, the producers writing
     x^T / dy straight into the pair buffers) == the unpaired loop (PICO_WGRAD_PAIR=0): the loss bit for bit (the
     forward is unchanged), every gradient / main_grad within fp32-summation tolerance; eager and pipelined graph,
-    with and without DataParallelBucket (RCCL, W = 1), even and odd grad_acc; hidden 1024 so the RMSNorm's y^T
-    form (a pair producer) runs. Also checks that the pairing happened: per step, every pair of micro-batches
-    defers 4 GEMMs per layer and pairs them."""
+    with and without DataParallelBucket (RCCL, W = 1), even and odd grad_acc, groups of 2 and 4 micro-batches
+    per GEMM (PICO_WGRAD_GROUP; a last partial group runs over its r slots); hidden 1024 so the RMSNorm's y^T
+    form (a pair producer) runs. Also checks that the grouping happened: per step, every group of r > 1
+    micro-batches defers (r - 1) x 4 GEMMs per layer and runs 4 group GEMMs."""
     import torch.distributed as dist
     from picotron_amd import process_group_manager as pgm
     from picotron_amd import wgrad_pair as WP
@@ -295,6 +298,7 @@ def test_wgrad_pairs_match_unpaired(monkeypatch, n, dp, graph):
         pgm.setup_process_group_manager(1, 1, 1, 1)
     try:
         res = {}
+        monkeypatch.setenv("PICO_WGRAD_GROUP", str(group))
         for mode in ("0", "1"):
             monkeypatch.setenv("PICO_WGRAD_PAIR", mode)
             torch.manual_seed(7)
@@ -325,13 +329,76 @@ def test_wgrad_pairs_match_unpaired(monkeypatch, n, dp, graph):
             res[mode] = (loss, grads, d)
         assert res["0"][0] == res["1"][0], (res["0"][0], res["1"][0])
         assert res["0"][2] == {"deferred": 0, "paired": 0}
-        pairs = (n // 2) * 4 * cfg.num_hidden_layers
+        L4 = 4 * cfg.num_hidden_layers
+        want = {"deferred": sum((min(group, n - g0) - 1) * L4 for g0 in range(0, n, group)),
+                "paired": sum(L4 for g0 in range(0, n, group) if n - g0 > 1)}
         if graph:  # decisions are taken while capturing (warm-up + capture), replays run no Python
-            assert res["1"][2]["paired"] >= pairs and res["1"][2]["deferred"] == res["1"][2]["paired"], res["1"][2]
+            got = res["1"][2]
+            assert got["paired"] >= want["paired"] and got["deferred"] >= want["deferred"], (got, want)
+            assert got["deferred"] * want["paired"] == got["paired"] * want["deferred"], (got, want)
         else:
-            assert res["1"][2] == {"deferred": pairs, "paired": pairs}, res["1"][2]
+            assert res["1"][2] == want, (res["1"][2], want)
         for nme in res["0"][1]:
             assert rel_l2(res["1"][1][nme].float().cpu(), res["0"][1][nme].float().cpu()) < 5e-3, nme
+    finally:
+        if dp:
+            pgm.process_group_manager = None
+            dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n,dp", [(4, False), (5, False), (4, True)])
+def test_wgrad_stream_matches_slot_streams(monkeypatch, n, dp):
+    """The pipelined graph's weight-gradient stream (ops.wgrad_stream: the paired wgrad GEMMs on a third stream,
+    pair-buffer producers on the capture stream waiting for the GEMM that last read the half they overwrite) ==
+    the same graph with every GEMM on its micro-batch's stream (PICO_WGRAD_STREAM=0): the same GEMMs on the same
+    operands in the same order, so the loss bit for bit and every gradient / main_grad to fp32 rounding, over two
+    steps (the second a replay). Even and odd grad_acc, with and without DataParallelBucket (RCCL, W = 1)."""
+    import torch.distributed as dist
+    from picotron_amd import process_group_manager as pgm
+    from picotron_amd.data import SyntheticDataLoader
+    from picotron_amd.data_parallel.data_parallel import DataParallelBucket
+    from picotron_amd.model import LlamaConfig, build_llama
+    from picotron_amd.train import PipelinedMicroBatchGraph, train_step
+    from conftest import rel_l2
+    cfg = LlamaConfig(**_PAIR_CFG)
+    if dp:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0", WORLD_SIZE="1",
+                          LOCAL_RANK="0")
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+        pgm.setup_process_group_manager(1, 1, 1, 1)
+    try:
+        res = {}
+        for mode in ("0", "1"):
+            monkeypatch.setenv("PICO_WGRAD_STREAM", mode)
+            torch.manual_seed(7)
+            m = build_llama(cfg, "cuda", BF)
+            with torch.no_grad():
+                m.final_proj.weight.normal_(0, 0.02, generator=torch.Generator("cuda").manual_seed(1))
+            model = DataParallelBucket(m, bucket_cap_mb=1) if dp else m
+            loader = SyntheticDataLoader(2, 128, n, cfg.vocab_size, seed=5, num_batches=2 * n, device="cuda")
+            for p in m.parameters():
+                p.grad = torch.zeros_like(p)
+
+            def zero():
+                for p in m.parameters():
+                    if p.grad is not None:
+                        p.grad.zero_()
+                if dp:
+                    model.bucket_manager.reset()
+            g = PipelinedMicroBatchGraph(model, n, zero)
+            losses = []
+            for _ in range(2):
+                zero()
+                losses.append(train_step(model, loader, "cuda", graphs=g))
+            torch.cuda.synchronize()
+            grads = {nme: (p.main_grad.clone() if dp else p.grad.float().clone()) for nme, p in m.named_parameters()}
+            res[mode] = (losses, grads)
+            del g
+        assert res["0"][0] == res["1"][0], (res["0"][0], res["1"][0])
+        exact = sum(int(torch.equal(res["0"][1][k], res["1"][1][k])) for k in res["0"][1])
+        print(f"[wgrad-stream] n={n} dp={dp}: {exact}/{len(res['0'][1])} gradients bit-identical", flush=True)
+        for k in res["0"][1]:
+            assert rel_l2(res["1"][1][k].float().cpu(), res["0"][1][k].float().cpu()) < 1e-6, k
     finally:
         if dp:
             pgm.process_group_manager = None
