@@ -377,7 +377,12 @@ class Llama(nn.Module):
             delta, residual = layer.forward_fused(delta, residual, prev_down=down)
             hints = layer._pair_hints()
             down = hints["down"] if hints else None
-        pair = (None, down) if down is not None else None
+        # the fused LM head + CE (return_hidden) groups its weight gradient too: the final norm's y^T goes into the
+        # head's x^T group slot (wgrad_pair)
+        head = getattr(self, "final_proj", None)
+        lm = (head.weight, head.weight.shape[0], head.weight.shape[1]) if (
+            return_hidden and down is not None and type(head) is nn.Linear and head.bias is None) else None
+        pair = (lm, down) if down is not None else None
         h = self.final_norm(delta, _pair=pair) if residual is None else \
             self.final_norm(delta, residual=residual, _pair=pair)
         if return_hidden:

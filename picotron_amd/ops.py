@@ -935,7 +935,7 @@ class _LMHeadCEChunkedFn(torch.autograd.Function):
         loss_rows = torch.empty(T, dtype=torch.float32, device=x.device)
         dx = torch.empty(T, H, dtype=x.dtype, device=x.device)
         chunk = max(1, min(int(chunk), T))
-        buf = torch.empty(chunk, V, dtype=x.dtype, device=x.device)
+        buf = None
         wt = weight_t(w, (w,)) if wt_dgrad_enabled() else None
         xin = _wgrad_input(x2, V, x)  # x2, or x2^T's transposed view ("TT" wgrad form)
         need_w = ctx.needs_input_grad[1]
@@ -955,6 +955,16 @@ class _LMHeadCEChunkedFn(torch.autograd.Function):
                     kind, dst = "grad", g
         lib = _lib.load()
         conc = "lm" in _conc_tags() and not _NO_SIDE[0]
+        # grouped weight gradient (wgrad_pair's groups, one chunk per micro-batch): the logits / dlogits go into the
+        # weight's dy group slot and x^T sits in its x^T slot (the final norm writes it there), and the dW GEMM runs
+        # once per group, over K = r T, in the group's last micro-batch (PICO_LM_WGRAD_GROUP=0: per micro-batch)
+        from . import wgrad_pair as WP
+        grouped = (need_w and chunk >= T and kind in ("main", "grad") and WP.active()
+                   and os.getenv("PICO_LM_WGRAD_GROUP", "1") != "0")
+        if grouped:
+            buf = WP.dy_out(w, V, H, T, x.dtype, x.device)
+        if buf is None:
+            buf = torch.empty(chunk, V, dtype=x.dtype, device=x.device)
         for c0 in range(0, T, chunk):
             c1 = min(T, c0 + chunk)
             n = c1 - c0
@@ -970,7 +980,15 @@ class _LMHeadCEChunkedFn(torch.autograd.Function):
             if conc and need_w:
                 side = _side_stream(x.device)
                 side.wait_stream(torch.cuda.current_stream(x.device))
-            if need_w:
+            if need_w and grouped:
+                plan = WP.plan(w, lg, xin)
+                if plan[0] == "gemm":
+                    with (torch.cuda.stream(side) if side is not None else contextlib.nullcontext()):
+                        if kind == "main":  # the group's sum in one fp32 GEMM, 1/W folded in when syncing
+                            torch.addmm(dst, plan[1].t(), plan[2], beta=sc, alpha=sc, out_dtype=torch.float32, out=dst)
+                        else:
+                            torch.addmm(dst, plan[1].t(), plan[2], out=dst)
+            elif need_w:
                 xc = xin[c0:c1]
                 with (torch.cuda.stream(side) if side is not None else contextlib.nullcontext()):
                     if kind == "main":  # fp32 main_grad: 1/W folds into the first chunk's beta and every alpha

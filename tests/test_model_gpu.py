@@ -281,7 +281,7 @@ def test_wgrad_pairs_match_unpaired(monkeypatch, n, dp, graph, group):
     with and without DataParallelBucket (RCCL, W = 1), even and odd grad_acc, groups of 2 and 4 micro-batches
     per GEMM (PICO_WGRAD_GROUP; a last partial group runs over its r slots); hidden 1024 so the RMSNorm's y^T
     form (a pair producer) runs. Also checks that the grouping happened: per step, every group of r > 1
-    micro-batches defers (r - 1) x 4 GEMMs per layer and runs 4 group GEMMs."""
+    micro-batches defers (r - 1) x 4 GEMMs per layer (+ 1 for the LM head) and runs 4 group GEMMs per layer (+ 1)."""
     import torch.distributed as dist
     from picotron_amd import process_group_manager as pgm
     from picotron_amd import wgrad_pair as WP
@@ -329,7 +329,7 @@ def test_wgrad_pairs_match_unpaired(monkeypatch, n, dp, graph, group):
             res[mode] = (loss, grads, d)
         assert res["0"][0] == res["1"][0], (res["0"][0], res["1"][0])
         assert res["0"][2] == {"deferred": 0, "paired": 0}
-        L4 = 4 * cfg.num_hidden_layers
+        L4 = 4 * cfg.num_hidden_layers + 1  # four projections per layer and the LM head (fused CE, one chunk)
         want = {"deferred": sum((min(group, n - g0) - 1) * L4 for g0 in range(0, n, group)),
                 "paired": sum(L4 for g0 in range(0, n, group) if n - g0 > 1)}
         if graph:  # decisions are taken while capturing (warm-up + capture), replays run no Python
