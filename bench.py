@@ -45,9 +45,12 @@ def pmc_traffic(kernel_name):
         return None, None
     with open(files[-1]) as fh:
         recs = json.load(fh)
-    for k, rec in recs.items():
-        if k.startswith(kernel_name + "_kernel<") and "traffic_bytes" in rec:
-            return round(rec["traffic_bytes"]), os.path.relpath(files[-1], ROOT) + ": " + k
+    # the device kernels behind a launch id, newest form first (attn_bwd_kv: the 64-row kernel for D = 64)
+    forms = {"attn_bwd_kv": ("attn_bwd_kvp_kernel<", "attn_bwd_kv_kernel<")}.get(kernel_name, (kernel_name + "_kernel<",))
+    for form in forms:
+        for k, rec in recs.items():
+            if k.startswith(form) and "traffic_bytes" in rec:
+                return round(rec["traffic_bytes"]), os.path.relpath(files[-1], ROOT) + ": " + k
     return None, None
 
 
