@@ -156,11 +156,10 @@ PICO_DEV void tr_offsets(int lane, unsigned (&tro)[D / 32][2]) {
 // ------------------------------------------------------------------------------------------------
 // dQ kernel (query-major)
 // ------------------------------------------------------------------------------------------------
-// PIPE (D = 64, opt-in PICO_ATTN_QP=1, round 5): the tile's two 32-key halves as one hand-ordered stream of 24
-// MFMA slots instead of one after the other — M1(h0) | h1's K / V fragments, M1(h1) | V(h0) and h0's transposed
-// K operands, M2(h0) | V(h1), M2(h1) — at two workgroups per CU (<= 256 VGPRs; as attn_bwd_kvp_kernel).
-template <int D, bool CAUSAL, bool PIPE = false>
-__global__ __launch_bounds__(256, PIPE ? 2 : QCfg<D>::MINB) void attn_bwd_q_kernel(const pico_attn_args a, float scale, float scale_log2,
+// (Round 5 measured and removed a pipelined form of this tile — the two 32-key halves as one hand-ordered stream
+// of 24 MFMA slots at two workgroups per CU, as attn_bwd_kvp_kernel: C2 40.5 vs 40.6 us, profiles/r05_ab_kvp_qp.jsonl.)
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(256, QCfg<D>::MINB) void attn_bwd_q_kernel(const pico_attn_args a, float scale, float scale_log2,
                                                              float* __restrict__ lse2_g, float* __restrict__ delta_g,
                                                              int sq_pad, unsigned long long* __restrict__ stamp_out,
                                                              int nfront, float lse_mul, float lse_pad) {
@@ -348,144 +347,6 @@ __global__ __launch_bounds__(256, PIPE ? 2 : QCfg<D>::MINB) void attn_bwd_q_kern
       }
     }
   };
-  // The pipelined tile (PIPE): one element pair of a half's softmax per slot (2 fma, 2 exp, 2 mul, 1 cvt_pk of
-  // dS^T), KVP-style sched_barrier fences between slots; every operand read two or more slots before its MFMA.
-  auto tile_p = [&](const char* kb, bool mask, int n0, int dtile, int dslot) __attribute__((always_inline)) {
-    static_assert(!PIPE || D == 64, "the pipelined dQ tile is written for D = 64");
-    const char* vb = kb + C::IMG;
-    bf16x8 k0[KS], v0[KS], k1[KS], v1[KS];
-    bf16x8 t0[2][DT], t1[2][DT];
-    unsigned w0[8], w1[8];
-    f32x16 s0, d0, s1, d1;
-    auto vp = [&](const f32x16& sv, const f32x16& dv, int e, unsigned& w) __attribute__((always_inline)) {
-      typedef __attribute__((ext_vector_type(2))) float f32x2;
-      typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
-      const float a0 = fast_exp2(__builtin_fmaf(sv[2 * e], scale_log2, nl2)) * dv[2 * e];
-      const float a1 = fast_exp2(__builtin_fmaf(sv[2 * e + 1], scale_log2, nl2)) * dv[2 * e + 1];
-      w = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){a0, a1}, bf16x2));
-    };
-    auto pk4 = [&](const unsigned* w) __attribute__((always_inline)) {
-      typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
-      return __builtin_bit_cast(bf16x8, (u32x4){w[0], w[1], w[2], w[3]});
-    };
-    auto minit = [&](int kt) __attribute__((always_inline)) {
-      f32x16 m;
-      if (mask) {
-        const int rel = lim_lane - n0 - 4 * h;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) m[i] = (32 * kt + (i & 3) + 8 * (i >> 2)) <= rel ? 0.f : -INFINITY;
-      } else {
-        m = (f32x16)0.f;
-      }
-      return m;
-    };
-#define QP_SLOT() __builtin_amdgcn_sched_barrier(0)
-    k0[0] = lds_read_b128(kb, ro[0]);
-    k0[1] = lds_read_b128(kb, ro[1]);
-    s0 = minit(0);
-    d0 = ndelta;
-    QP_SLOT();
-    s0 = mfma32(k0[0], qf[0], s0);  // a1
-    k0[2] = lds_read_b128(kb, ro[2]);
-    k0[3] = lds_read_b128(kb, ro[3]);
-    QP_SLOT();
-    s0 = mfma32(k0[1], qf[1], s0);  // a2
-    v0[0] = lds_read_b128(vb, ro[0]);
-    v0[1] = lds_read_b128(vb, ro[1]);
-    QP_SLOT();
-    s0 = mfma32(k0[2], qf[2], s0);  // a3
-    v0[2] = lds_read_b128(vb, ro[2]);
-    v0[3] = lds_read_b128(vb, ro[3]);
-    QP_SLOT();
-    s0 = mfma32(k0[3], qf[3], s0);  // a4
-    k1[0] = lds_read_b128(kb, ro[0] + 32 * RB);
-    k1[1] = lds_read_b128(kb, ro[1] + 32 * RB);
-    QP_SLOT();
-    d0 = mfma32(v0[0], df[0], d0);  // a5
-    k1[2] = lds_read_b128(kb, ro[2] + 32 * RB);
-    k1[3] = lds_read_b128(kb, ro[3] + 32 * RB);
-    QP_SLOT();
-    d0 = mfma32(v0[1], df[1], d0);  // a6
-    v1[0] = lds_read_b128(vb, ro[0] + 32 * RB);
-    v1[1] = lds_read_b128(vb, ro[1] + 32 * RB);
-    QP_SLOT();
-    d0 = mfma32(v0[2], df[2], d0);  // a7
-    v1[2] = lds_read_b128(vb, ro[2] + 32 * RB);
-    v1[3] = lds_read_b128(vb, ro[3] + 32 * RB);
-    QP_SLOT();
-    d0 = mfma32(v0[3], df[3], d0);  // a8
-    s1 = minit(1);
-    d1 = ndelta;
-    QP_SLOT();
-    s1 = mfma32(k1[0], qf[0], s1);  // b1
-    t0[0][0] = tr_pair(kb, tro[0][0], tro[0][1]);
-    QP_SLOT();
-    s1 = mfma32(k1[1], qf[1], s1);  // b2
-    t0[0][1] = tr_pair(kb, tro[1][0], tro[1][1]);
-    QP_SLOT();
-    s1 = mfma32(k1[2], qf[2], s1);  // b3
-    vp(s0, d0, 0, w0[0]);
-    QP_SLOT();
-    s1 = mfma32(k1[3], qf[3], s1);  // b4
-    vp(s0, d0, 1, w0[1]);
-    QP_SLOT();
-    d1 = mfma32(v1[0], df[0], d1);  // b5
-    vp(s0, d0, 2, w0[2]);
-    t0[1][0] = tr_pair(kb + 16 * RB, tro[0][0], tro[0][1]);
-    QP_SLOT();
-    d1 = mfma32(v1[1], df[1], d1);  // b6
-    vp(s0, d0, 3, w0[3]);
-    t0[1][1] = tr_pair(kb + 16 * RB, tro[1][0], tro[1][1]);
-    QP_SLOT();
-    d1 = mfma32(v1[2], df[2], d1);  // b7
-    vp(s0, d0, 4, w0[4]);
-    QP_SLOT();
-    d1 = mfma32(v1[3], df[3], d1);  // b8
-    vp(s0, d0, 5, w0[5]);
-    QP_SLOT();
-    const bf16x8 ds00 = pk4(w0);
-    dq[0] = mfma32(t0[0][0], ds00, dq[0]);  // c1
-    vp(s0, d0, 6, w0[6]);
-    t1[0][0] = tr_pair(kb + 32 * RB, tro[0][0], tro[0][1]);
-    QP_SLOT();
-    dq[1] = mfma32(t0[0][1], ds00, dq[1]);  // c2
-    vp(s0, d0, 7, w0[7]);
-    t1[0][1] = tr_pair(kb + 32 * RB, tro[1][0], tro[1][1]);
-    QP_SLOT();
-    const bf16x8 ds01 = pk4(w0 + 4);
-    dq[0] = mfma32(t0[1][0], ds01, dq[0]);  // c3
-    vp(s1, d1, 0, w1[0]);
-    vp(s1, d1, 1, w1[1]);
-    QP_SLOT();
-    dq[1] = mfma32(t0[1][1], ds01, dq[1]);  // c4
-    vp(s1, d1, 2, w1[2]);
-    vp(s1, d1, 3, w1[3]);
-    t1[1][0] = tr_pair(kb + 48 * RB, tro[0][0], tro[0][1]);
-    t1[1][1] = tr_pair(kb + 48 * RB, tro[1][0], tro[1][1]);
-    QP_SLOT();
-    const bf16x8 ds10 = pk4(w1);
-    dq[0] = mfma32(t1[0][0], ds10, dq[0]);  // d1
-    vp(s1, d1, 4, w1[4]);
-    vp(s1, d1, 5, w1[5]);
-    if (dtile >= 0) issue_piece(dtile, dslot, 0);
-    QP_SLOT();
-    dq[1] = mfma32(t1[0][1], ds10, dq[1]);  // d2
-    vp(s1, d1, 6, w1[6]);
-    vp(s1, d1, 7, w1[7]);
-    if (dtile >= 0) issue_piece(dtile, dslot, 1);
-    QP_SLOT();
-    const bf16x8 ds11 = pk4(w1 + 4);
-    dq[0] = mfma32(t1[1][0], ds11, dq[0]);  // d3
-    if (dtile >= 0) issue_piece(dtile, dslot, 2);
-    QP_SLOT();
-    dq[1] = mfma32(t1[1][1], ds11, dq[1]);  // d4
-    if (dtile >= 0) {
-      issue_piece(dtile, dslot, 3);
-      bump();
-    }
-    QP_SLOT();
-#undef QP_SLOT
-  };
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // prologue tiles and loads landed
 #if PICO_BWDQ_WGSTAMP
   wgs[1] = __builtin_amdgcn_s_memrealtime();
@@ -503,14 +364,8 @@ __global__ __launch_bounds__(256, PIPE ? 2 : QCfg<D>::MINB) void attn_bwd_q_kern
       lds_barrier();  // every wave's pieces of tile t visible; slot (t + P) % NBUF no longer read
       const int n0 = t * KT;
       const bool busy = n0 <= lim_last;  // wave-uniform: some row of the wave sees some key of the tile
-      if constexpr (PIPE) {
-        // the pipelined tile issues the DMA of tile t + P in its M2 gaps (one piece per slot; see tile_p)
-        if (t + P < ntiles && !busy) issue(t + P, (u + P) % C::NBUF);
-        if (busy) tile_p(smem + u * C::SLOT, n0 + KT - 1 > lim_first, n0, t + P < ntiles ? t + P : -1, (u + P) % C::NBUF);
-      } else {
-        if (t + P < ntiles) issue(t + P, (u + P) % C::NBUF);
-        if (busy) tile(smem + u * C::SLOT, n0 + KT - 1 > lim_first, n0);
-      }
+      if (t + P < ntiles) issue(t + P, (u + P) % C::NBUF);
+      if (busy) tile(smem + u * C::SLOT, n0 + KT - 1 > lim_first, n0);
     }
   }
 
@@ -1472,11 +1327,6 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kvp_kernel(const pico
 #undef KVP_ST
 #undef KVP_SLOT
 
-bool qp_enabled() {
-  const char* e = getenv("PICO_ATTN_QP");
-  return e && e[0] == '1';
-}
-
 // attn_bwd_kvp_kernel (64-row tiles, two workgroups per CU) for D = 64 up to 2048 keys, the 32-row kernel beyond:
 // same box, 3 interleaved rounds (profiles/r05_ab_kvp_default.jsonl): dK/dV C2 55.2 -> 53.5 us, GQA-4 57.4 -> 53.2,
 // C2 non-causal 76.7 -> 72.7, but S 4096 138.8 -> 147.2. PICO_ATTN_KVP=0 / 1 forces it off / on (A/B switch).
@@ -1531,10 +1381,7 @@ int q_front(const pico_attn_args* a) {
   if (!a->causal) return 0;
   const int nmb = (int)((a->seqlen_q + QB - 1) / QB);
   const int64_t nbh = a->batch * a->heads_q;
-  int minb = a->head_dim == 64 ? QCfg<64>::MINB : QCfg<128>::MINB;
-#ifndef PICO_SPLIT_D128_TU
-  if (a->head_dim == 64 && qp_enabled()) minb = 2;  // the pipelined tile: two workgroups per CU
-#endif
+  const int minb = a->head_dim == 64 ? QCfg<64>::MINB : QCfg<128>::MINB;
   const int64_t first = (int64_t)pico_num_cus() * minb / (nbh > 0 ? nbh : 1);  // groups resident at once
   return first < nmb ? (int)(nmb - first) : 0;
 }
@@ -1617,14 +1464,6 @@ int launch_split(const pico_attn_args* a, hipStream_t s) {
   const int nmb = (int)((a->seqlen_q + QB - 1) / QB);
   const int64_t gq = (int64_t)nmb * a->batch * a->heads_q;
   PICO_REQUIRE(gq < (1ll << 31), "pico_attn_bwd: grid too large");
-#ifndef PICO_SPLIT_D128_TU
-  if (D == 64 && qp_enabled())
-    PICO_TRY(pico_launch(PICO_K_ATTN_BWD_Q, "attn_bwd_q", attn_bwd_q_kernel<D, CAUSAL, true>, dim3((int)gq), dim3(256), 0, s,
-                         *a, a->softmax_scale, sl2, lse2, delta, sq_pad,
-                         (unsigned long long*)((char*)a->workspace + pico_attn_bwd_split_workspace(a) - STAMP_BYTES),
-                         q_front(a), use_kvp ? -1.0f / a->softmax_scale : LOG2E, use_kvp ? -INFINITY : INFINITY));
-  else
-#endif
   PICO_TRY(pico_launch(PICO_K_ATTN_BWD_Q, "attn_bwd_q", attn_bwd_q_kernel<D, CAUSAL>, dim3((int)gq), dim3(256), 0, s,
                        *a, a->softmax_scale, sl2, lse2, delta, sq_pad,
                        (unsigned long long*)((char*)a->workspace + pico_attn_bwd_split_workspace(a) - STAMP_BYTES),

@@ -369,16 +369,6 @@ def wgrad_fusion_enabled():
     return os.getenv("PICO_WGRAD_FUSION", "1") != "0"
 
 
-def _dp_stacked_mode():
-    """PICO_DP_STACKED: how the row-stacked parameters' (q|k|v, gate|up) weight gradients reach their fp32
-    main_grads under DataParallelBucket — "gemm" (one fp32-output GEMM per parameter into its main_grad) or
-    "accum" (one bf16 GEMM over the stack, then pico_grad_accum per parameter: the reference's bf16 dW + hook
-    sequence; the default: per-parameter fp32 GEMMs measured slower, C2 step at W = 1 870.2 -> 875.6 ms, 3 rounds,
-    profiles/r05_ab_dp_stacked.jsonl — the fp32 epilogue's read-modify-write sits inside the GEMM instead of in a
-    separate pass the other micro-batch's work overlaps)."""
-    return os.getenv("PICO_DP_STACKED", "accum")
-
-
 def wgrad_accumulate(params, dy2, x2):
     """dW = dy2^T x2 for row-stacked `params` ([sum rows, K]); returns the grads for autograd
     (None where the GEMM already accumulated into the parameter's gradient storage)."""
@@ -405,20 +395,8 @@ def wgrad_accumulate(params, dy2, x2):
         # the forward that first uses the parameter, so in the two-stream pipelined graph (forward i + 1 beside
         # backward i) the node of micro-batch i served micro-batch i + 1 too, and torch synchronised the two
         # streams on every such gradient ("AccumulateGrad node's stream does not match ...").
-        if _dp_stacked_mode() == "gemm":
-            # one fp32-output GEMM per parameter on its rows of dy (a column slice of dy2: no copy), accumulating
-            # into main_grad in the GEMM's epilogue as the single-parameter branch above does — no bf16 dW
-            # buffer and no separate accumulate pass over main_grad
-            r0 = 0
-            for p in params:
-                n = p.shape[0]
-                sync, world = p._pico_wgrad_sync()
-                sc = 1.0 / world if sync else 1.0
-                torch.addmm(p.main_grad, dy2[:, r0:r0 + n].t(), x2, beta=sc, alpha=sc, out_dtype=torch.float32,
-                            out=p.main_grad)
-                p._pico_wgrad_ready()
-                r0 += n
-            return (None,) * len(params)
+        # (one fp32-output GEMM per parameter on its column slice of dy measured slower: the fp32 read-modify-write
+        # then sits in the GEMM's epilogue instead of a pass the other micro-batch's work overlaps)
         from .data_parallel.bucket import get_kernels
         buf = torch.mm(dy2.t(), x2)
         r0 = 0
@@ -625,34 +603,6 @@ def _side_stream(dev):
     return side
 
 
-_WSTREAM = [None]  # the pipelined graph's weight-gradient stream while it issues its micro-batches
-
-
-@contextlib.contextmanager
-def wgrad_stream(stream, origin):
-    """Within (PipelinedMicroBatchGraph's body): the paired weight-gradient GEMMs run on `stream`, off the
-    micro-batches' dgrad chains — each waits for an event recorded where its operands are complete and runs in
-    issue order (every gradient accumulates in micro-batch order); the pair-buffer producers on `origin` wait for
-    the GEMM that last read the half they overwrite (wgrad_pair.reader_stream). The caller joins `stream` into
-    `origin` at the end."""
-    from . import wgrad_pair as WP
-    prev = _WSTREAM[0]
-    _WSTREAM[0] = stream
-    try:
-        with WP.reader_stream(origin):
-            yield
-    finally:
-        _WSTREAM[0] = prev
-
-
-def wgrad_stream_enabled():
-    """PICO_WGRAD_STREAM=1: the pipelined graph runs its weight-gradient GEMMs on a third stream (ops.wgrad_stream).
-    Off by default: measured slower, C2 step 834.8 -> 874.0 ms (DataParallelBucket 864.1 -> 897.9), 2 alternating
-    rounds on one box (profiles/r05_ab_wgrad_stream.jsonl) — a third stream of GEMMs beside the two micro-batches
-    splits the chip three ways, and the backward chain's own GEMMs then run on what is left of it."""
-    return os.getenv("PICO_WGRAD_STREAM", "0") == "1"
-
-
 def _wgrad_paired(params, dy2, x2):
     """wgrad_accumulate with paired weight gradients (wgrad_pair): the first micro-batch of a pair whose operands
     sit in the pair buffers defers its GEMM (a DP readiness callback still marks the parameter as produced by a
@@ -665,25 +615,6 @@ def _wgrad_paired(params, dy2, x2):
             if ready is not None and getattr(p, "main_grad", None) is not None:
                 ready()
         return (None,) * len(params)
-    w = _WSTREAM[0]
-    if w is not None and plan[1].is_cuda and not any(
-            getattr(p, "_pico_wgrad_sync", None) is not None and p._pico_wgrad_sync()[0] for p in params):
-        # on the wgrad stream (never for a DP-syncing micro-batch: its bucket readiness is recorded on the
-        # compute stream)
-        cur = torch.cuda.current_stream(plan[1].device)
-        ev = torch.cuda.Event()
-        ev.record(cur)
-        w.wait_event(ev)
-        for t in (plan[1], plan[2]):
-            t.record_stream(w)
-        with torch.cuda.stream(w):
-            res = wgrad_accumulate(params, plan[1], plan[2])
-            done = torch.cuda.Event()
-            done.record(w)
-        WP.note_reader(params[0], WP._CTX["i"], done)
-        if any(r is not None for r in res):
-            cur.wait_event(done)  # a gradient handed to autograd: its consumers run on this stream
-        return res
     return wgrad_accumulate(params, plan[1], plan[2])
 
 
@@ -701,9 +632,6 @@ def dgrad_wgrad(tag, dy2, W, params, x2):
         dx = dgrad(dy2, W, params)
         cur.wait_stream(side)
         return dx, dws
-    if _WSTREAM[0] is not None:  # the wgrad stream takes over as soon as the operands are complete
-        dws = _wgrad_paired(params, dy2, x2)
-        return dgrad(dy2, W, params), dws
     return dgrad(dy2, W, params), _wgrad_paired(params, dy2, x2)
 
 

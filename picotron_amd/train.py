@@ -233,16 +233,10 @@ class PipelinedMicroBatchGraph:
         # segfaults on this ROCm (scripts/dbg_event_capture.py reproduces it with plain tensor ops)
         streams = (cur, self.streams[1])
         streams[1].wait_stream(cur)
-        # the paired weight-gradient GEMMs on a third stream (ops.wgrad_stream), joined at the end: off the
-        # backward chain, beside its HBM-bound kernels and the other slot's work
-        wst = self.streams[2] if ops.wgrad_stream_enabled() and WP.enabled() else None
-        if wst is not None:
-            wst.wait_stream(cur)
-        with (ops.wgrad_stream(wst, cur) if wst is not None else contextlib.nullcontext()):
-            self._slots(model, n, acc, streams, inp, tgt)
+        # (a third stream for the grouped weight-gradient GEMMs, waits routed through the capture stream, measured
+        # 4.7 % slower: DESIGN.md §4e)
+        self._slots(model, n, acc, streams, inp, tgt)
         cur.wait_stream(streams[1])
-        if wst is not None:
-            cur.wait_stream(wst)
 
     def _slots(self, model, n, acc, streams, inp, tgt):
         from . import ops
@@ -274,8 +268,7 @@ class PipelinedMicroBatchGraph:
     def _capture(self, batches):
         dev = batches[0][0].device
         if self.streams is None:
-            # slot 0: the caller's (capture) stream; slot 1; the weight-gradient stream
-            self.streams = (None, torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev))
+            self.streams = (None, torch.cuda.Stream(device=dev))  # slot 0: the caller's (capture) stream
         inp = torch.stack([b[0] for b in batches])
         tgt = torch.stack([b[1] for b in batches])
         if self.loss_acc is None:

@@ -103,10 +103,6 @@ class PairBuf:
         self.dy = torch.empty((G * T, N), dtype=dtype, device=device)
         # (x^T set, next slot) of a group whose first members deferred their GEMM to its last member, or None
         self.pending = None
-        # events recorded after the last weight-gradient GEMM that read these buffers on another stream (the
-        # pipelined graph's wgrad stream): a producer on the capture stream waits for them before overwriting
-        self.xt_reader = [None, None]
-        self.dy_reader = None
 
     def xt_slot(self, i):
         """Micro-batch i's x^T: [K, T] view, row stride G T, in set (i // G) % 2, columns of slot i % G."""
@@ -116,49 +112,6 @@ class PairBuf:
     def dy_slot(self, i):
         h = i % self.G
         return self.dy[h * self.T:(h + 1) * self.T]
-
-
-# (stream, origin stream) while the pipelined graph issues its weight-gradient GEMMs on a stream of their own
-_READERS = {"origin": None}
-
-
-@contextlib.contextmanager
-def reader_stream(origin):
-    """Within: the wgrad GEMMs may read the pair buffers on another stream (note_reader); producers on `origin`
-    (the capture stream) wait for the last such read of the half they overwrite. Producers on the other pipeline
-    slot do not wait: each follows a producer of the same buffer on `origin` through the slots' event chain (a
-    direct wait would put dependencies both ways between two forked capture streams, which this ROCm's
-    hipStreamEndCapture does not survive). Reader events never outlive the context."""
-    _clear_readers()
-    prev = _READERS["origin"]
-    _READERS["origin"] = origin
-    try:
-        yield
-    finally:
-        _READERS["origin"] = prev
-        _clear_readers()
-
-
-def _clear_readers():
-    for _, b in list(_BUFS.values()):
-        b.xt_reader = [None, None]
-        b.dy_reader = None
-
-
-def note_reader(weight, i, event):
-    """The wgrad GEMM of `weight` issued for micro-batch i read its pair buffers (dy, and x^T set (i // 2) % 2) on
-    another stream, done at `event`."""
-    b = _get(weight)
-    if b is None or _READERS["origin"] is None:
-        return
-    b.xt_reader[(i // b.G) % 2] = event
-    b.dy_reader = event
-
-
-def _wait_reader(ev):
-    o = _READERS["origin"]
-    if ev is not None and o is not None and torch.cuda.current_stream(o.device) == o:
-        o.wait_event(ev)
 
 
 def buf(weight, N, K, T, dtype, device):
@@ -180,9 +133,7 @@ def xt_out(weight, N, K, T, dtype, device):
     stride 2T), or None when pairing is off."""
     if not active() or weight is None:
         return None
-    b = buf(weight, N, K, T, dtype, device)
-    _wait_reader(b.xt_reader[(_CTX["i"] // b.G) % 2])
-    return b.xt_slot(_CTX["i"])
+    return buf(weight, N, K, T, dtype, device).xt_slot(_CTX["i"])
 
 
 def dy_out(weight, N, K, T, dtype, device):
@@ -190,9 +141,7 @@ def dy_out(weight, N, K, T, dtype, device):
     contiguous), or None when pairing is off."""
     if not active() or weight is None:
         return None
-    b = buf(weight, N, K, T, dtype, device)
-    _wait_reader(b.dy_reader)
-    return b.dy_slot(_CTX["i"])
+    return buf(weight, N, K, T, dtype, device).dy_slot(_CTX["i"])
 
 
 def dy_out_existing(weight, N, K, T, dtype, device):
@@ -203,7 +152,6 @@ def dy_out_existing(weight, N, K, T, dtype, device):
     b = _get(weight)
     if b is None or (b.N, b.K, b.T) != (N, K, T) or b.dy.dtype != dtype or b.dy.device != device:
         return None
-    _wait_reader(b.dy_reader)
     return b.dy_slot(_CTX["i"])
 
 
@@ -231,7 +179,6 @@ def dy_out_if_paired(weight, x2, N, K, T, dtype, device):
     b = _get(weight)
     if b is None or (b.N, b.K, b.T) != (N, K, T) or x2.data_ptr() != b.xt_slot(_CTX["i"]).data_ptr():
         return None
-    _wait_reader(b.dy_reader)
     return b.dy_slot(_CTX["i"])
 
 
@@ -258,7 +205,6 @@ def plan(weight, dy2, x2):
                            "failed step left)")
     if h > 0 and b.pending == (s, h):
         if not mine:
-            _wait_reader(b.dy_reader)
             b.dy_slot(i).copy_(dy2)
             b.xt_slot(i).copy_(x2.t())
         if h < r - 1:

@@ -346,65 +346,6 @@ def test_wgrad_pairs_match_unpaired(monkeypatch, n, dp, graph, group):
             dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("n,dp", [(4, False), (5, False), (4, True)])
-def test_wgrad_stream_matches_slot_streams(monkeypatch, n, dp):
-    """The pipelined graph's weight-gradient stream (ops.wgrad_stream: the paired wgrad GEMMs on a third stream,
-    pair-buffer producers on the capture stream waiting for the GEMM that last read the half they overwrite) ==
-    the same graph with every GEMM on its micro-batch's stream (PICO_WGRAD_STREAM=0): the same GEMMs on the same
-    operands in the same order, so the loss bit for bit and every gradient / main_grad to fp32 rounding, over two
-    steps (the second a replay). Even and odd grad_acc, with and without DataParallelBucket (RCCL, W = 1)."""
-    import torch.distributed as dist
-    from picotron_amd import process_group_manager as pgm
-    from picotron_amd.data import SyntheticDataLoader
-    from picotron_amd.data_parallel.data_parallel import DataParallelBucket
-    from picotron_amd.model import LlamaConfig, build_llama
-    from picotron_amd.train import PipelinedMicroBatchGraph, train_step
-    from conftest import rel_l2
-    cfg = LlamaConfig(**_PAIR_CFG)
-    if dp:
-        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0", WORLD_SIZE="1",
-                          LOCAL_RANK="0")
-        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
-        pgm.setup_process_group_manager(1, 1, 1, 1)
-    try:
-        res = {}
-        for mode in ("0", "1"):
-            monkeypatch.setenv("PICO_WGRAD_STREAM", mode)
-            torch.manual_seed(7)
-            m = build_llama(cfg, "cuda", BF)
-            with torch.no_grad():
-                m.final_proj.weight.normal_(0, 0.02, generator=torch.Generator("cuda").manual_seed(1))
-            model = DataParallelBucket(m, bucket_cap_mb=1) if dp else m
-            loader = SyntheticDataLoader(2, 128, n, cfg.vocab_size, seed=5, num_batches=2 * n, device="cuda")
-            for p in m.parameters():
-                p.grad = torch.zeros_like(p)
-
-            def zero():
-                for p in m.parameters():
-                    if p.grad is not None:
-                        p.grad.zero_()
-                if dp:
-                    model.bucket_manager.reset()
-            g = PipelinedMicroBatchGraph(model, n, zero)
-            losses = []
-            for _ in range(2):
-                zero()
-                losses.append(train_step(model, loader, "cuda", graphs=g))
-            torch.cuda.synchronize()
-            grads = {nme: (p.main_grad.clone() if dp else p.grad.float().clone()) for nme, p in m.named_parameters()}
-            res[mode] = (losses, grads)
-            del g
-        assert res["0"][0] == res["1"][0], (res["0"][0], res["1"][0])
-        exact = sum(int(torch.equal(res["0"][1][k], res["1"][1][k])) for k in res["0"][1])
-        print(f"[wgrad-stream] n={n} dp={dp}: {exact}/{len(res['0'][1])} gradients bit-identical", flush=True)
-        for k in res["0"][1]:
-            assert rel_l2(res["1"][1][k].float().cpu(), res["0"][1][k].float().cpu()) < 1e-6, k
-    finally:
-        if dp:
-            pgm.process_group_manager = None
-            dist.destroy_process_group()
-
-
 def _train_grads(cfg, toks, fusion, monkeypatch, dp=None):
     """grad_acc = len(toks) micro-batches; returns {name: fp32 grad (or main_grad with DP)}."""
     from picotron_amd.model import build_llama
