@@ -112,17 +112,18 @@ struct KVCfg {
 // the dQ kernel's query blocks measured slower (C2 42.8 -> 47.3 us, GQA-4 40.0 -> 43.9: its lightest-first front,
 // q_front, frees slots early for the heavy blocks, which a one-round grid cannot), so the dQ grid stays plain.
 // grp.n == 0: the plain grid, one block per workgroup.
+constexpr int GRP_MAX = 16;  // groups per (batch, head)
 struct BlkGroups {
-  int n;          // groups per (batch, head); 0 = one block per workgroup
-  unsigned cnt;   // blocks in group g: nibble g (1..4)
-  unsigned w[8];  // block ids of group g: byte j of w[g], j < its count (heaviest first)
+  int n;                   // groups per (batch, head); 0 = one block per workgroup
+  unsigned long long cnt;  // blocks in group g: nibble g (1..4)
+  unsigned w[GRP_MAX];     // block ids of group g: byte j of w[g], j < its count (heaviest first)
 };
 
 // w[g] for a wave-uniform g without indexing the kernel-argument array (selects, no scratch copy)
 PICO_DEV unsigned grp_sel(const BlkGroups& t, int g) {
   unsigned r = t.w[0];
 #pragma unroll
-  for (int i = 1; i < 8; ++i) r = g == i ? t.w[i] : r;
+  for (int i = 1; i < GRP_MAX; ++i) r = g == i ? t.w[i] : r;
   return r;
 }
 
@@ -453,7 +454,7 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kv_kernel(const pico_
   const int b = bh / (int)a.heads_kv, hk = bh % (int)a.heads_kv;
   // the group's key blocks one after the other (grp.n == 0: the one block gi)
   const unsigned gw = grp.n ? grp_sel(grp, gi) : 0u;
-  const int nblk_wg = grp.n ? (int)((grp.cnt >> (4 * gi)) & 15u) : 1;
+  const int nblk_wg = grp.n ? (int)((grp.cnt >> (4 * gi)) & 15ull) : 1;
 #pragma clang loop unroll(disable)
   for (int jb = 0; jb < nblk_wg; ++jb) {
   const int kb = grp.n ? (int)((gw >> (8 * jb)) & 255u) : gi;
@@ -916,7 +917,7 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kvp_kernel(const pico
   const int bh = bhs / hsplit;
   const int b = bh / (int)a.heads_kv, hk = bh % (int)a.heads_kv;
   const unsigned gw = grp.n ? grp_sel(grp, gi) : 0u;
-  const int nblk_wg = grp.n ? (int)((grp.cnt >> (4 * gi)) & 15u) : 1;
+  const int nblk_wg = grp.n ? (int)((grp.cnt >> (4 * gi)) & 15ull) : 1;
   const unsigned delta_off = (unsigned)((const char*)delta_g - (const char*)sinit_g);  // same workspace
   const unsigned ring_lds = (unsigned)__builtin_amdgcn_readfirstlane((int)lds_addr(smem));
 #pragma clang loop unroll(disable)
@@ -1327,15 +1328,17 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kvp_kernel(const pico
 #undef KVP_ST
 #undef KVP_SLOT
 
-// attn_bwd_kvp_kernel (64-row tiles, two workgroups per CU) for D = 64 up to 2048 keys, the 32-row kernel beyond:
-// same box, 3 interleaved rounds (profiles/r05_ab_kvp_default.jsonl): dK/dV C2 55.2 -> 53.5 us, GQA-4 57.4 -> 53.2,
-// C2 non-causal 76.7 -> 72.7, but S 4096 138.8 -> 147.2. PICO_ATTN_KVP=0 / 1 forces it off / on (A/B switch).
+// attn_bwd_kvp_kernel (64-row tiles, two workgroups per CU) for D = 64 up to 2048 keys (4096 non-causal), the
+// 32-row kernel beyond: same box, 3 interleaved rounds (profiles/r05_ab_kvp_default.jsonl, r05_ab_kvp_long.jsonl):
+// dK/dV C2 55.2 -> 53.5 us, GQA-4 57.4 -> 53.2, C2 non-causal 76.7 -> 72.7, S 2048 (B 2) 81.0 -> 81.3, S 4096
+// non-causal (config 5's off-diagonal ring blocks) 266.7 -> 255.5, but S 4096 causal 138.5 -> 144.7.
+// PICO_ATTN_KVP=0 / 1 forces it off / on (A/B switch).
 bool kvp_enabled(const pico_attn_args* a) {
   if (a->head_dim != 64) return false;
   const char* e = getenv("PICO_ATTN_KVP");
   if (e && e[0] == '0') return false;
   if (e && e[0] == '1') return true;
-  return a->seqlen_k <= 2048;
+  return a->seqlen_k <= (a->causal ? 2048 : 4096);
 }
 #endif  // !PICO_SPLIT_D128_TU
 
@@ -1404,10 +1407,10 @@ BlkGroups block_groups(const int* wt, int nblk, int64_t nbh, int minb) {
   const int64_t slots = (int64_t)minb * cus;
   if (!groups_enabled() || nbh <= 0 || nblk > 32 || (int64_t)nblk * nbh <= slots) return t;
   const int G = (int)(slots / nbh);
-  if (G < 2 || G > 8 || nblk > 4 * G) return t;
+  if (G < 2 || G > GRP_MAX || nblk > 4 * G) return t;
   static const double spd[3] = {1.0, 0.75, 0.53};
-  double tgt[8], load[8] = {0.0}, tot = 0.0, ssum = 0.0;
-  int cnt[8] = {0};
+  double tgt[GRP_MAX], load[GRP_MAX] = {0.0}, tot = 0.0, ssum = 0.0;
+  int cnt[GRP_MAX] = {0};
   for (int i = 0; i < nblk; ++i) tot += wt[i];
   for (int g = 0; g < G; ++g) {
     const int cls = (int)std::min<int64_t>(minb - 1, (int64_t)g * nbh / cus);
@@ -1430,7 +1433,7 @@ BlkGroups block_groups(const int* wt, int nblk, int64_t nbh, int minb) {
   }
   for (int g = 0; g < G; ++g) {
     if (cnt[g] == 0) return BlkGroups{};
-    t.cnt |= (unsigned)cnt[g] << (4 * g);
+    t.cnt |= (unsigned long long)cnt[g] << (4 * g);
   }
   t.n = G;
   return t;

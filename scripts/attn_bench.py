@@ -22,6 +22,8 @@ CONFIGS = {
     "d128_b2": (2, 1024, 16, 16, 128, True),   # the same at micro-batch 2 (half the work: one 256-CU round)
     "gqa4": (4, 1024, 32, 8, 64, True),
     "s4096": (1, 4096, 32, 32, 64, True),   # CP block size of config 5
+    "s4096_full": (1, 4096, 32, 32, 64, False),  # config 5's off-diagonal ring blocks
+    "s2048": (2, 2048, 32, 32, 64, True),
     "d128_full": (4, 1024, 16, 16, 128, False),
     "d128_s4096": (1, 4096, 16, 16, 128, True),
     "d128_gqa4": (4, 1024, 32, 8, 128, True),

@@ -20,6 +20,8 @@ CASES = {  # B, S, Hq, Hkv, D, causal
     "ragged": (1, 1000, 4, 4, 64, True),
     "gqa4": (4, 1024, 32, 8, 64, True),
     "s4096": (1, 4096, 32, 32, 64, True),
+    "s4096_full": (1, 4096, 8, 8, 64, False),
+    "s3000": (1, 3000, 8, 4, 64, True),
     "full": (2, 1024, 8, 8, 64, False),
     "fold5": (6, 640, 32, 32, 64, True),      # 5 blocks x 192 heads > one round: one folded pair per head
     "fold_ragged": (7, 1000, 32, 32, 64, True),  # ragged last block inside a folded pair
