@@ -880,8 +880,8 @@ struct KVPCfg {
 
 #define KVP_SLOT() __builtin_amdgcn_sched_barrier(0)
 
-template <bool CAUSAL, int MINB>
-__global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kvp_kernel(const pico_attn_args a, float scale, float c2,
+template <bool CAUSAL, int MINB, int NW>
+__global__ __launch_bounds__(NW * 64, MINB) void attn_bwd_kvp_kernel(const pico_attn_args a, float scale, float c2,
                                                                 const float* __restrict__ sinit_g,
                                                                 const float* __restrict__ delta_g, int sq_pad,
                                                                 int hsplit, float* __restrict__ dkv_part,
@@ -902,7 +902,10 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kvp_kernel(const pico
 #define KVP_ST(i)
 #endif
   constexpr int KS = C::KS, DT = C::DT, CPR = C::CPR, RB = C::RB;
-  static_assert(C::NP == 4 * KNW + 1, "four Q / dO pieces per wave + one LSE / delta piece");
+  // NW waves x 32 keys per block; each wave issues PPW of a tile's 16 image pieces (the first half Q, the second
+  // dO), wave 0 also the LSE / delta piece
+  constexpr int PPW = 2 * C::NQP / NW, KB = 32 * NW;
+  static_assert(C::NP == PPW * NW + 1 && (PPW == 2 || PPW == 4), "Q / dO pieces per wave + one LSE / delta piece");
   __shared__ __attribute__((aligned(16))) char smem[C::NBUF * C::SLOT];
 
   const int lane0 = threadIdx.x & 63;
@@ -930,7 +933,7 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kvp_kernel(const pico
   int lane_l = lane0;
   asm volatile("" : "+v"(lane_l));
   const int lane = lane_l, r = lane & 31, h = lane >> 5;
-  const int k0 = kb * KVB;
+  const int k0 = kb * KB;
   const int kw = k0 + 32 * wave;
   const int qstart = CAUSAL ? k0 : 0;  // k0 is a multiple of QT2
   const int nqt = Sq > qstart ? (Sq - qstart + QT2 - 1) / QT2 : 0;
@@ -945,13 +948,13 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kvp_kernel(const pico
   const int64_t qs1 = a.q_strides[1] * 2, ds1 = a.do_strides[1] * 2;  // bytes per query row
   const char* const qbase = (const char*)((const bf16_t*)a.q + b * a.q_strides[0]);
   const char* const dobase = (const char*)((const bf16_t*)a.dout + b * a.do_strides[0]);
-  int pc_row[4];
-  unsigned pc_off[4];
+  int pc_row[PPW];
+  unsigned pc_off[PPW];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int jj = (wave + 4 * i) % C::NQP;
+  for (int i = 0; i < PPW; ++i) {
+    const int jj = (wave + NW * i) % C::NQP;
     pc_row[i] = C::RPP * jj + lane / CPR;
-    pc_off[i] = (unsigned)(pc_row[i] * (i < 2 ? qs1 : ds1) + 8 * ((lane % CPR) ^ swz<64>(pc_row[i])) * 2);
+    pc_off[i] = (unsigned)(pc_row[i] * (i < PPW / 2 ? qs1 : ds1) + 8 * ((lane % CPR) ^ swz<64>(pc_row[i])) * 2);
   }
   struct Tc {
     int hq, q0;
@@ -980,20 +983,20 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kvp_kernel(const pico
     }
   };
   const bool ragged = Sq % QT2 != 0;
-  // one of this wave's pieces of a tile: i < 4 the image pieces, i == 4 the LSE / delta piece (wave 0 only)
+  // one of this wave's pieces of a tile: i < PPW the image pieces, i == PPW the LSE / delta piece (wave 0 only)
   auto issue_piece = [&](int si, const Tc& c, int i) __attribute__((always_inline)) {
     const unsigned dst = ring_lds + (unsigned)si * (unsigned)C::SLOT;
-    if (i < 4) {
-      const int jj = (wave + 4 * i) % C::NQP;
+    if (i < PPW) {
+      const int jj = (wave + NW * i) % C::NQP;
       unsigned off = pc_off[i];
       if (ragged && c.q0 + QT2 > Sq) {  // partial tile: rows past Sq - 1 clamped (finite; their LSE is +inf)
         int l2 = lane0;
         asm volatile("" : "+v"(l2));
         const int row = C::RPP * jj + (l2 & 63) / CPR;
-        off = (unsigned)((min(c.q0 + row, Sq - 1) - c.q0) * (i < 2 ? qs1 : ds1) +
+        off = (unsigned)((min(c.q0 + row, Sq - 1) - c.q0) * (i < PPW / 2 ? qs1 : ds1) +
                          8 * (((l2 & 63) % CPR) ^ swz<64>(row)) * 2);
       }
-      dma_piece(i < 2 ? c.qp : c.dp, off, dst + (i < 2 ? 0u : (unsigned)C::QIMG) + (unsigned)jj * 1024u);
+      dma_piece(i < PPW / 2 ? c.qp : c.dp, off, dst + (i < PPW / 2 ? 0u : (unsigned)C::QIMG) + (unsigned)jj * 1024u);
     } else if (wave == 0) {
       int l = lane0;
       asm volatile("" : "+v"(l));
@@ -1003,7 +1006,7 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kvp_kernel(const pico
   };
   auto issue = [&](int si, const Tc& c) __attribute__((always_inline)) {
 #pragma unroll
-    for (int i = 0; i < 5; ++i) issue_piece(si, c, i);
+    for (int i = 0; i <= PPW; ++i) issue_piece(si, c, i);
   };
   Tc nxt = make_tc(hq0, q00);
 #pragma unroll
@@ -1084,7 +1087,7 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kvp_kernel(const pico
       if (t > 0) {
         // this wave's pieces of tile t landed; those of the younger tiles already issued stay in flight
         const int younger = min(C::PD - 1, ntiles - 1 - t);
-        wait_vmcnt(younger * (wave == 0 ? 5 : 4));
+        wait_vmcnt(younger * (wave == 0 ? PPW + 1 : PPW));
         KVP_ST(0);
         lds_barrier();  // every wave's pieces of tile t visible; the slot of tile t - 1 is no longer read
         KVP_ST(1);
@@ -1249,10 +1252,10 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kvp_kernel(const pico
       if (dma_next) issue_piece(DSLOT, nxt, 2);
       KVP_SLOT();
       dk[0] = mfma32(tqB[1][0], sB1, dk[0]);  // d6
-      if (dma_next) issue_piece(DSLOT, nxt, 3);
+      if (PPW > 2 && dma_next) issue_piece(DSLOT, nxt, 3);
       KVP_SLOT();
       dv[1] = mfma32(toB[1][1], pB1, dv[1]);  // d7
-      if (dma_next) issue_piece(DSLOT, nxt, 4);
+      if (PPW > 2 && dma_next) issue_piece(DSLOT, nxt, 4);
       KVP_SLOT();
       dk[1] = mfma32(tqB[1][1], sB1, dk[1]);  // d8
       advance(nxt);
@@ -1319,28 +1322,49 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kvp_kernel(const pico
 #if PICO_KVP_STAMP
   ph[11] = __builtin_amdgcn_s_memrealtime();
   ph[13] = __builtin_amdgcn_s_memtime();
-  if ((threadIdx.x & 63) == 0 && blockIdx.x < 8192) {
+  if ((threadIdx.x & 63) == 0 && (int64_t)blockIdx.x * NW + wave < STAMP_BYTES / 128) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) stamp_out[((int64_t)blockIdx.x * 4 + wave) * 16 + i] = ph[i];
+    for (int i = 0; i < 16; ++i) stamp_out[((int64_t)blockIdx.x * NW + wave) * 16 + i] = ph[i];
   }
 #endif
 }
 #undef KVP_ST
 #undef KVP_SLOT
 
-// attn_bwd_kvp_kernel (64-row tiles, two workgroups per CU) for D = 64 up to 2048 keys (4096 non-causal), the
-// 32-row kernel beyond: same box, 3 interleaved rounds (profiles/r05_ab_kvp_default.jsonl, r05_ab_kvp_long.jsonl):
-// dK/dV C2 55.2 -> 53.5 us, GQA-4 57.4 -> 53.2, C2 non-causal 76.7 -> 72.7, S 2048 (B 2) 81.0 -> 81.3, S 4096
-// non-causal (config 5's off-diagonal ring blocks) 266.7 -> 255.5, but S 4096 causal 138.5 -> 144.7.
-// PICO_ATTN_KVP=0 / 1 forces it off / on (A/B switch).
+// attn_bwd_kvp_kernel (64-row tiles) for D = 64 up to 1536 causal / 4096 non-causal keys, the 32-row kernel beyond.
+// Same box, 3 interleaved rounds each (profiles/r05_ab_kvp_default.jsonl, r05_ab_kvp_long.jsonl,
+// r05_ab_kvp_waves.jsonl): dK/dV C2 55.2 -> 53.5 us, GQA-4 57.4 -> 53.2, C2 non-causal 76.7 -> 72.7, S 4096
+// non-causal (config 5's off-diagonal ring blocks) 266.7 -> 255.5; at S 2048 causal the two kernels measured equal
+// on one box (81.3 vs 81.0) and 91.0 vs 95.7 on another, at S 4096 causal 138.5 vs 144.7 and 143.7 vs 150.6.
+// PICO_ATTN_KVP=0 / 1 forces either (A/B switch).
 bool kvp_enabled(const pico_attn_args* a) {
   if (a->head_dim != 64) return false;
   const char* e = getenv("PICO_ATTN_KVP");
   if (e && e[0] == '0') return false;
   if (e && e[0] == '1') return true;
-  return a->seqlen_k <= (a->causal ? 2048 : 4096);
+  return a->seqlen_k <= (a->causal ? 1536 : 4096);
+}
+
+// waves (x 32 keys) per attn_bwd_kvp_kernel workgroup: 4 (two 128-key workgroups per CU), or 8 (one 256-key
+// workgroup per CU: each Q / dO tile loaded and each barrier taken once for twice the keys) for non-causal blocks of
+// 2048 keys and more: S 4096 non-causal 259.8 -> 256.8 us; at C2 shapes 8 waves lose (C2 52.9 -> 57.9, GQA-4
+// 53.1 -> 65.5: a 256-workgroup grid is too coarse there). PICO_KVP_WAVES=4 / 8 forces either (A/B switch).
+int kvp_waves(const pico_attn_args* a) {
+  const char* e = getenv("PICO_KVP_WAVES");
+  if (e && atoi(e) == 8) return 8;
+  if (e && atoi(e) == 4) return 4;
+  return !a->causal && a->seqlen_k >= 2048 ? 8 : 4;
 }
 #endif  // !PICO_SPLIT_D128_TU
+
+// keys per dK/dV workgroup block
+int kv_block(const pico_attn_args* a) {
+#ifndef PICO_SPLIT_D128_TU
+  if (kvp_enabled(a)) return 32 * kvp_waves(a);
+#endif
+  (void)a;
+  return KVB;
+}
 
 // rows of the LSE / delta workspace per (batch, head): padded to the 64-row tiles of attn_bwd_kvp_kernel
 int split_sq_pad(const pico_attn_args* a) { return (int)((a->seqlen_q + 63) / 64) * 64; }
@@ -1358,7 +1382,7 @@ int64_t split_lsd_floats(const pico_attn_args* a) {
 int kv_minb(const pico_attn_args* a) {
   if (a->head_dim == 128) return 1;
 #ifndef PICO_SPLIT_D128_TU
-  if (kvp_enabled(a)) return 2;  // attn_bwd_kvp_kernel: two waves per SIMD, <= 256 VGPRs
+  if (kvp_enabled(a)) return kvp_waves(a) == 8 ? 1 : 2;  // attn_bwd_kvp_kernel: two waves per SIMD, <= 256 VGPRs
 #endif
   return a->causal ? 3 : 2;
 }
@@ -1367,7 +1391,8 @@ int kv_minb(const pico_attn_args* a) {
 // C2 at MINB 3: kv + dkv 55.5 + 13.8 us with 4 parts, 67.2 + 9.6 with 2, 62.1 + 9.7 at MINB 2)
 int kv_hsplit(const pico_attn_args* a) {
   if (a->heads_kv <= 0 || a->heads_q % a->heads_kv != 0) return 1;
-  const int64_t nblk = ((a->seqlen_k + KVB - 1) / KVB) * a->batch * a->heads_kv;
+  const int kvb = kv_block(a);
+  const int64_t nblk = ((a->seqlen_k + kvb - 1) / kvb) * a->batch * a->heads_kv;
   const int64_t tiles = (a->heads_q / a->heads_kv) * ((a->seqlen_q + QT - 1) / QT);
   if (nblk <= 0) return 1;
   int d = 1;
@@ -1442,11 +1467,12 @@ BlkGroups block_groups(const int* wt, int nblk, int64_t nbh, int minb) {
 // dK/dV kernel groups: key block kb sees (Hq / Hkv) * ceil((Sq - 128 kb) / 32) query tiles (causal, no hsplit)
 BlkGroups kv_groups(const pico_attn_args* a, int hsplit, int minb) {
   if (!a->causal || hsplit != 1 || a->heads_kv <= 0) return BlkGroups{};
-  const int nkb = (int)((a->seqlen_k + KVB - 1) / KVB);
+  const int kvb = kv_block(a);
+  const int nkb = (int)((a->seqlen_k + kvb - 1) / kvb);
   if (nkb > 32) return BlkGroups{};
   int wt[32];
   for (int kb = 0; kb < nkb; ++kb) {
-    const int64_t q0 = (int64_t)kb * KVB;
+    const int64_t q0 = (int64_t)kb * kvb;
     wt[kb] = (int)((a->heads_q / a->heads_kv) * (a->seqlen_q > q0 ? (a->seqlen_q - q0 + QT - 1) / QT : 0));
   }
   return block_groups(wt, nkb, a->batch * a->heads_kv, minb);
@@ -1471,16 +1497,20 @@ int launch_split(const pico_attn_args* a, hipStream_t s) {
                        *a, a->softmax_scale, sl2, lse2, delta, sq_pad,
                        (unsigned long long*)((char*)a->workspace + pico_attn_bwd_split_workspace(a) - STAMP_BYTES),
                        q_front(a), use_kvp ? -1.0f / a->softmax_scale : LOG2E, use_kvp ? -INFINITY : INFINITY));
-  const int nkb = (int)((a->seqlen_k + KVB - 1) / KVB);
+  const int nkb = (int)((a->seqlen_k + kv_block(a) - 1) / kv_block(a));
   const int hsplit = kv_hsplit(a);
   const BlkGroups kg = kv_groups(a, hsplit, kv_minb(a));
   const int64_t nblk = (int64_t)(kg.n ? kg.n : nkb) * a->batch * a->heads_kv * hsplit;
   if (nblk == 0) return 0;
   unsigned long long* stamps = (unsigned long long*)((char*)a->workspace + pico_attn_bwd_split_workspace(a) - STAMP_BYTES);
 #ifndef PICO_SPLIT_D128_TU
-  if (use_kvp) {
-    PICO_TRY(pico_launch(PICO_K_ATTN_BWD_KV, "attn_bwd_kv", attn_bwd_kvp_kernel<CAUSAL, 2>, dim3((int)nblk),
-                         dim3(KNW * 64), 0, s, *a, a->softmax_scale, sl2, lse2, delta, sq_pad, hsplit, dkv_part, kg,
+  if (use_kvp && kvp_waves(a) == 8) {
+    PICO_TRY(pico_launch(PICO_K_ATTN_BWD_KV, "attn_bwd_kv", attn_bwd_kvp_kernel<CAUSAL, 1, 8>, dim3((int)nblk),
+                         dim3(8 * 64), 0, s, *a, a->softmax_scale, sl2, lse2, delta, sq_pad, hsplit, dkv_part, kg,
+                         stamps));
+  } else if (use_kvp) {
+    PICO_TRY(pico_launch(PICO_K_ATTN_BWD_KV, "attn_bwd_kv", attn_bwd_kvp_kernel<CAUSAL, 2, 4>, dim3((int)nblk),
+                         dim3(4 * 64), 0, s, *a, a->softmax_scale, sl2, lse2, delta, sq_pad, hsplit, dkv_part, kg,
                          stamps));
   } else
 #endif

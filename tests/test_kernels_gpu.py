@@ -419,15 +419,16 @@ def test_attention_bwd_d128_key_block_groups(S, Hq, Hkv, causal, mode):
     (2, 1024, 1024, 8, 8, True, "bf16"),     # C2 slice, block groups
     (1, 1000, 1000, 8, 2, True, "bf16"),     # ragged, GQA 4
     (4, 1024, 1024, 32, 8, True, "bf16"),    # GQA 4 at a small grid: key blocks split over workgroups (hsplit)
-    (1, 2048, 2048, 4, 4, True, "rope"),     # the default's last length, fused RoPE^-1
+    (1, 1536, 1536, 4, 4, True, "rope"),     # the causal default's last length, fused RoPE^-1
     (1, 2049, 2049, 2, 2, True, "f32acc"),   # past it (default: the 32-row kernel), caller's fp32 dQ
+    (1, 2048, 2048, 4, 4, False, "bf16"),    # non-causal 2048: the 8-wave default
     (2, 96, 200, 4, 4, False, "bf16"),       # cross lengths, non-causal
     (1, 640, 640, 4, 4, False, "rope"),
 ])
 def test_attention_bwd_d64_kv_kernels(monkeypatch, B, Sq, Sk, Hq, Hkv, causal, mode):
-    """D = 64 dK/dV: attn_bwd_kvp_kernel (64-row query tiles; the default up to 2048 keys) and the 32-row
-    attn_bwd_kv_kernel (PICO_ATTN_KVP=0 / 1 force either), each with its matching dQ-kernel LSE form, vs an fp32 torch
-    reference, and the two within bf16 rounding of each other."""
+    """D = 64 dK/dV: attn_bwd_kvp_kernel (64-row query tiles, 4 or 8 waves x 32 keys per workgroup: the default up
+    to 4096 keys) and the 32-row attn_bwd_kv_kernel (PICO_ATTN_KVP=0 / 1 and PICO_KVP_WAVES=4 / 8 force each), each
+    with its matching dQ-kernel LSE form, vs an fp32 torch reference, and within bf16 rounding of each other."""
     from picotron_amd.model import get_cos_sin
     ops = _ops()
     torch.manual_seed(Sq * 3 + Sk + Hq + Hkv)
@@ -454,8 +455,9 @@ def test_attention_bwd_d64_kv_kernels(monkeypatch, B, Sq, Sk, Hq, Hkv, causal, m
         ops._rope_launch(gk.to(BF).contiguous(), rk, cos, sin, True)
         gq, gk = rq.float(), rk.float()
     res = {}
-    for kvp in ("0", "1"):
-        monkeypatch.setenv("PICO_ATTN_KVP", kvp)
+    for kvp in ("0", "1", "1w8"):
+        monkeypatch.setenv("PICO_ATTN_KVP", kvp[0])
+        monkeypatch.setenv("PICO_KVP_WAVES", "8" if kvp.endswith("w8") else "4")
         if mode == "bf16":
             dq, dk, dv = ops.attention_block_bwd(do, q, k, v, o, lse, sc, causal)
         elif mode == "f32acc":
@@ -469,8 +471,9 @@ def test_attention_bwd_d64_kv_kernels(monkeypatch, B, Sq, Sk, Hq, Hkv, causal, m
         res[kvp] = [t.float() for t in (dq, dk, dv)]
         for a, b in zip(res[kvp], (gq, gk, gv)):
             assert rel_l2(a, b) < 1e-2, (kvp, rel_l2(a, b))
-    for a, b in zip(res["0"], res["1"]):
-        assert rel_l2(a, b) < 8e-3
+    for other in ("1", "1w8"):
+        for a, b in zip(res["0"], res[other]):
+            assert rel_l2(a, b) < 8e-3
 
 
 def test_attention_dq_f32_accumulate():
