@@ -849,18 +849,19 @@ __global__ __launch_bounds__(KNW * 64, MINB) void attn_bwd_kv_kernel(const pico_
 
 #ifndef PICO_SPLIT_D128_TU
 // ------------------------------------------------------------------------------------------------
-// dK / dV kernel, D = 64, 64-row query tiles in a hand-ordered stream (round 5; PICO_ATTN_KVP)
+// dK / dV kernel, D = 64, 64-row query tiles in a hand-ordered stream (round 5; the default up to 1536 causal /
+// 4096 non-causal keys, kvp_enabled)
 // ------------------------------------------------------------------------------------------------
-// The same work as attn_bwd_kv_kernel (key on the lane, 32 keys per wave, 128 keys per workgroup, K / V fragments
-// resident), but each ring tile is 64 query rows, two 32-row halves A and B whose phases interleave inside one
+// The same work as attn_bwd_kv_kernel (key on the lane, 32 keys per wave, NW = 4 or 8 waves = 128 or 256 keys per
+// workgroup, K / V fragments resident), but each ring tile is 64 query rows, two 32-row halves A and B whose phases interleave inside one
 // wave: M1 = S and dP (8 MFMAs per half), V = the softmax VALU (P = exp2(c S'), dS = P dP, packed to bf16), M2 =
 // dV^T += dO^T P and dK^T += Q^T dS (8 MFMAs per half). The 32-row kernel's tile is one dependency chain
 // (M1 -> V -> M2, every operand read right before its MFMA: 19 waits per tile, ~1 us per tile for a wave
 // alone); here a tile is the stream
 //     M1(A) | reads of B's operands,  M1(B) | V(A) + A's transposed reads,  M2(A) | V(B) + B's reads,  M2(B)
 // so every MFMA gap carries independent work (the guide's per-gap budget: <= 5 fillers, one transcendental),
-// one barrier and one DMA round serve 64 rows, and two waves per SIMD (two workgroups per CU, <= 256 VGPRs)
-// fill each other's remaining gaps. Row constants enter as the initial accumulators (no subtraction, no LSE
+// one barrier and one DMA round serve 64 rows, and two waves per SIMD (two 4-wave or one 8-wave workgroup per CU,
+// <= 256 VGPRs) fill each other's remaining gaps. Row constants enter as the initial accumulators (no subtraction, no LSE
 // registers): S' = Q K^T - LSE / scale (the dQ kernel writes -LSE / scale for these rows, -inf for padding
 // rows; the causal / padding-key mask sets -inf in that initial value on diagonal tiles) and dP' = dO V^T - delta.
 constexpr int QT2 = 64;
