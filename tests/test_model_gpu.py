@@ -346,6 +346,63 @@ def test_wgrad_pairs_match_unpaired(monkeypatch, n, dp, graph, group):
             dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("n,dp", [(8, False), (5, True)])
+def test_layer_ordered_backwards_match(monkeypatch, n, dp):
+    """PICO_LAYER_ORDER=1 (layer_order: in the pipelined graph, backward i enters each layer after backward i - 1
+    has left it, instead of starting after it ended) == the whole-backward order: the loss and every gradient /
+    main_grad bit for bit over two steps (capture + replay), groups of four micro-batches per wgrad GEMM, with and
+    without DataParallelBucket (RCCL, W = 1; its syncing micro-batch runs eagerly after the graph)."""
+    import torch.distributed as dist
+    from picotron_amd import process_group_manager as pgm
+    from picotron_amd.data import SyntheticDataLoader
+    from picotron_amd.data_parallel.data_parallel import DataParallelBucket
+    from picotron_amd.model import LlamaConfig, build_llama
+    from picotron_amd.train import PipelinedMicroBatchGraph, train_step
+    cfg = LlamaConfig(**_PAIR_CFG)
+    if dp:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0", WORLD_SIZE="1",
+                          LOCAL_RANK="0")
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+        pgm.setup_process_group_manager(1, 1, 1, 1)
+    try:
+        res = {}
+        monkeypatch.setenv("PICO_WGRAD_GROUP", "4")
+        for order in ("0", "1"):
+            monkeypatch.setenv("PICO_LAYER_ORDER", order)
+            torch.manual_seed(7)
+            m = build_llama(cfg, "cuda", BF)
+            with torch.no_grad():
+                m.final_proj.weight.normal_(0, 0.02, generator=torch.Generator("cuda").manual_seed(1))
+            model = DataParallelBucket(m, bucket_cap_mb=1) if dp else m
+            loader = SyntheticDataLoader(2, 128, n, cfg.vocab_size, seed=5, num_batches=2 * n, device="cuda")
+            for p in m.parameters():
+                p.grad = torch.zeros_like(p)
+
+            def zero():
+                for p in m.parameters():
+                    p.grad.zero_()
+                if dp:
+                    model.bucket_manager.reset()
+            g = PipelinedMicroBatchGraph(model, n, zero)
+            out = []
+            for _ in range(2):
+                zero()
+                loss = train_step(model, loader, "cuda", graphs=g)
+                torch.cuda.synchronize()
+                out.append((loss, {nme: (p.main_grad.clone() if dp else p.grad.clone())
+                                   for nme, p in m.named_parameters()}))
+            res[order] = out
+            del g, model, m
+        for (l0, g0), (l1, g1) in zip(res["0"], res["1"]):
+            assert l0 == l1, (l0, l1)
+            for nme in g0:
+                assert torch.equal(g0[nme], g1[nme]), nme
+    finally:
+        if dp:
+            pgm.process_group_manager = None
+            dist.destroy_process_group()
+
+
 def _train_grads(cfg, toks, fusion, monkeypatch, dp=None):
     """grad_acc = len(toks) micro-batches; returns {name: fp32 grad (or main_grad with DP)}."""
     from picotron_amd.model import build_llama
