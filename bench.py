@@ -160,6 +160,9 @@ def main():
                          "syncing micro-batch's bucket all-reduces and their exposure, on RCCL at W = 1)")
     ap.add_argument("--graphs", type=int, default=1,
                     help="replay non-syncing micro-batches as a HIP graph (1) or run them eagerly (0)")
+    ap.add_argument("--comm-steps", type=int, default=1,
+                    help="DataParallelBucket runs: untimed steps after the timed region that record the exposed "
+                         "all-reduce time (RCCL only; 0 = skip)")
     args = ap.parse_args()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         raise SystemExit(_spawn_workers(args.gpus))
@@ -224,9 +227,6 @@ def main():
         for k in kernel_ids:
             L.prof_enable(k, cap)
 
-    dp_timed = hasattr(model, "comm_timing")
-    if dp_timed:  # device events around the syncing micro-batch's bucket all-reduces (comm_exposure)
-        model.comm_timing(True)
     dist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
@@ -261,10 +261,20 @@ def main():
                 kernels[L.KERNEL_NAMES[k]] = {"total_ms": tot, "launches": n, "avg_us": 1e3 * tot / n}
         L.load().pico_prof_enable(0, 0)
 
+    # Exposed all-reduce time: device events around the syncing micro-batch's bucket all-reduces, over untimed steps
+    # AFTER the throughput region (the per-bucket events and waits stay out of the timed steps). Only on
+    # RCCL: gloo's Work.wait() blocks the host inside the backward, so its timings would describe the harness.
     exposure = None
-    if dp_timed:
-        exposure = comm_exposure(model.comm_report(), world, device)
-        model.comm_timing(False)
+    if hasattr(model, "comm_timing") and args.comm_steps > 0:
+        if dist.get_backend() == "nccl":
+            model.comm_timing(True)
+            for _ in range(args.comm_steps):
+                step(sync_loss=True)
+            torch.cuda.synchronize()
+            exposure = comm_exposure(model.comm_report(), world, device)
+            model.comm_timing(False)
+        else:
+            exposure = {"exposed_ms": None, "exposed_over": f"not measured: {dist.get_backend()} backend"}
     allreduce = measure_allreduce(model, world, device) if world > 1 else None
     if exposure is not None:
         allreduce = dict(allreduce or {"buckets": len(model.bucket_manager.buckets)}, **exposure)
@@ -360,7 +370,9 @@ def main():
                                     "pipelined graph (forward i beside backward i-1)" if pipelined_enabled() else
                                     "graph per micro-batch"),
                        "wgrad": ("grouped micro-batches (one GEMM per projection per %d micro-batches)" % _WP.group_size()
-                                 if _WP.enabled() and (not args.graphs or pipelined_enabled()) else "per micro-batch")},
+                                 if _WP.enabled() and (not args.graphs or pipelined_enabled()) else "per micro-batch"),
+                       "wgrad_group_buffers_gb": round(_WP.footprint_bytes() / 1e9, 2),
+                       "peak_memory_gb": round(torch.cuda.max_memory_allocated(device) / 1e9, 1)},
             "tokens_per_sec_per_gpu": round(tps_gpu, 1),
             "mfu_pct": round(mfu, 2),
             "mfu_peak_tflops": round(BF16_PEAK_TFLOPS, 1),
@@ -399,6 +411,10 @@ def comm_exposure(report, world, device):
     if not report:
         return None
     exp = sum(r["exposed_ms"] for r in report) / len(report)
+    # buckets that did not sync in some recorded pass (None timings) are left out of the means
+    nb0 = len(report[0]["buckets"])
+    keep = [i for i in range(nb0) if all(r["buckets"][i][0] is not None for r in report)]
+    report = [dict(r, buckets=[r["buckets"][i] for i in keep]) for r in report]
     t = torch.tensor([exp], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     nb = len(report[0]["buckets"])

@@ -86,6 +86,21 @@ const char* pico_last_error(void);
 int pico_prof_enable(int kernel_id, int capacity);
 int pico_prof_collect(int kernel_id, double* total_ms, int64_t* launches);
 
+/* ---- kernel selection (A/B switches; process-wide, read by every later launch) ----
+ * Each knob starts at its shipped default (PICO_SEL_AUTO = the library's shape rule), overridden ONCE, when the
+ * library is loaded, by the environment variable named beside it; pico_select(knob, value) sets it afterwards
+ * (value PICO_SEL_AUTO restores the rule). Returns the previous value, or -2 for an unknown knob. No launch reads
+ * the environment. */
+#define PICO_SEL_AUTO (-1)
+enum {
+  PICO_SEL_ATTN_KVP = 0,    /* PICO_ATTN_KVP: D=64 dK/dV kernel, 1 = 64-row attn_bwd_kvp_kernel, 0 = 32-row kernel */
+  PICO_SEL_KVP_WAVES = 1,   /* PICO_KVP_WAVES: waves per attn_bwd_kvp_kernel workgroup, 4 or 8 */
+  PICO_SEL_ATTN_GROUPS = 2, /* PICO_ATTN_GROUPS: one-round block groups of the causal dK/dV grid, 1 on / 0 off */
+  PICO_SEL_ATTN_FWD = 3,    /* PICO_ATTN_FWD: forward kernel, 1 = persistent 64-row-per-wave kernel, 0 = 32-row */
+  PICO_SEL_COUNT = 4
+};
+int pico_select(int knob, int value);
+
 /* ---- RMSNorm: y = x * rsqrt(mean(x^2) + eps) * w, fp32 math, one bf16 rounding ----
  * x, y: [rows, cols] bf16 row-major (row stride = cols); w: [cols] bf16; rstd: [rows] fp32 (saved
  * for backward). residual (optional, may be NULL): x_eff = bf16(x + residual), written to

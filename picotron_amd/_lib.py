@@ -28,6 +28,10 @@ KERNEL_NAMES = {
     K_ATTN_BWD_KV: "attn_bwd_kv", K_ATTN_BWD_Q: "attn_bwd_q",
 }
 
+# kernel-selection knobs (pico_select; PICO_SEL_* in include/picotron_hip.h)
+SEL_AUTO = -1
+SEL_ATTN_KVP, SEL_KVP_WAVES, SEL_ATTN_GROUPS, SEL_ATTN_FWD = 0, 1, 2, 3
+
 ATTN_DQ_F32_ACCUM = 1
 ATTN_ROPE_BWD = 2
 ATTN_ROPE_Q_FWD = 4
@@ -56,6 +60,7 @@ _SIGNATURES = {
     "pico_last_error": (ctypes.c_char_p, []),
     "pico_prof_enable": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
     "pico_prof_collect": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(c_i64)]),
+    "pico_select": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
     "pico_rmsnorm_fwd": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, ctypes.c_float, c_vp]),
     "pico_rmsnorm_fwd_t": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64,
                                           ctypes.c_float, c_vp]),
@@ -114,6 +119,9 @@ def load():
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
+        # the selection knobs take their environment values now, at load (the first pico_select initialises the
+        # table; the second puts the value back)
+        lib.pico_select(SEL_ATTN_KVP, lib.pico_select(SEL_ATTN_KVP, SEL_AUTO))
         _lib = lib
     return _lib
 
@@ -137,6 +145,15 @@ def ptr(t):
 
 def i64x3(vals):
     return (c_i64 * 3)(*[int(v) for v in vals])
+
+
+def select(knob: int, value: int) -> int:
+    """Set a kernel-selection knob (SEL_*; value SEL_AUTO = the library's shape rule); returns the previous value.
+    The environment variables of the same names are read once, when the library loads."""
+    old = load().pico_select(knob, value)
+    if old == -2:
+        raise ValueError(f"pico_select: unknown knob {knob}")
+    return old
 
 
 def prof_enable(kernel_id: int, capacity: int = 4096):

@@ -57,8 +57,9 @@ constexpr int QT = 32;                    // dkv kernel: query rows per tile
 #define PICO_BWDQ_WGSTAMP 0
 #endif
 // PICO_KVP_STAMP: diagnostic build — every wave of attn_bwd_kvp_kernel accumulates s_memtime (shader clock)
-// deltas per phase of its tiles (wait, barrier, DMA issue, M1(A), M1(B), M2(A), M2(B)) and the tile count:
-// 8 x 8 B per wave at stamp_out[(block * 4 + wave) * 8] (scripts/kvp_stamps.py)
+// deltas per phase of its tiles (wait, barrier, DMA issue, M1(A), M1(B), M2(A), M2(B)), the tile count, the block
+// prologue / epilogue cycles and the wave's start / end clocks: 16 x 8 B per wave at
+// stamp_out[(block * NW + wave) * 16] (NW = waves per workgroup; scripts/kvp_stamps.py)
 #ifndef PICO_KVP_STAMP
 #define PICO_KVP_STAMP 0
 #endif
@@ -1337,23 +1338,21 @@ __global__ __launch_bounds__(NW * 64, MINB) void attn_bwd_kvp_kernel(const pico_
 // r05_ab_kvp_waves.jsonl): dK/dV C2 55.2 -> 53.5 us, GQA-4 57.4 -> 53.2, C2 non-causal 76.7 -> 72.7, S 4096
 // non-causal (config 5's off-diagonal ring blocks) 266.7 -> 255.5; at S 2048 causal the two kernels measured equal
 // on one box (81.3 vs 81.0) and 91.0 vs 95.7 on another, at S 4096 causal 138.5 vs 144.7 and 143.7 vs 150.6.
-// PICO_ATTN_KVP=0 / 1 forces either (A/B switch).
+// pico_select(PICO_SEL_ATTN_KVP, 0 / 1) forces either (A/B switch).
 bool kvp_enabled(const pico_attn_args* a) {
   if (a->head_dim != 64) return false;
-  const char* e = getenv("PICO_ATTN_KVP");
-  if (e && e[0] == '0') return false;
-  if (e && e[0] == '1') return true;
+  const int e = pico_sel(PICO_SEL_ATTN_KVP);
+  if (e != PICO_SEL_AUTO) return e != 0;
   return a->seqlen_k <= (a->causal ? 1536 : 4096);
 }
 
 // waves (x 32 keys) per attn_bwd_kvp_kernel workgroup: 4 (two 128-key workgroups per CU), or 8 (one 256-key
 // workgroup per CU: each Q / dO tile loaded and each barrier taken once for twice the keys) for non-causal blocks of
 // 2048 keys and more: S 4096 non-causal 259.8 -> 256.8 us; at C2 shapes 8 waves lose (C2 52.9 -> 57.9, GQA-4
-// 53.1 -> 65.5: a 256-workgroup grid is too coarse there). PICO_KVP_WAVES=4 / 8 forces either (A/B switch).
+// 53.1 -> 65.5: a 256-workgroup grid is too coarse there). pico_select(PICO_SEL_KVP_WAVES, 4 / 8) forces either.
 int kvp_waves(const pico_attn_args* a) {
-  const char* e = getenv("PICO_KVP_WAVES");
-  if (e && atoi(e) == 8) return 8;
-  if (e && atoi(e) == 4) return 4;
+  const int e = pico_sel(PICO_SEL_KVP_WAVES);
+  if (e == 4 || e == 8) return e;
   return !a->causal && a->seqlen_k >= 2048 ? 8 : 4;
 }
 #endif  // !PICO_SPLIT_D128_TU
@@ -1415,11 +1414,8 @@ int q_front(const pico_attn_args* a) {
   return first < nmb ? (int)(nmb - first) : 0;
 }
 
-// PICO_ATTN_GROUPS=0 restores the plain causal grids (one block per workgroup; A/B switch)
-bool groups_enabled() {
-  const char* e = getenv("PICO_ATTN_GROUPS");
-  return !(e && e[0] == '0');
-}
+// pico_select(PICO_SEL_ATTN_GROUPS, 0) restores the plain causal grids (one block per workgroup; A/B switch)
+bool groups_enabled() { return pico_sel(PICO_SEL_ATTN_GROUPS) != 0; }
 
 // The one-round schedule of BlkGroups: the nblk blocks of each (batch, head) (work wt[i] in tiles) cut into
 // G = minb * CUs / nbh groups, so that the grid is exactly one round of minb workgroups per CU. Groups are

@@ -38,6 +38,8 @@ PICO_DEV unsigned pack2bf(float lo, float hi) {
 // ---------------------------------------------------------------------------------------
 int pico_set_error(const char* fmt, ...);
 int pico_check_launch(const char* op);
+// current value of a kernel-selection knob (PICO_SEL_*, pico_select; PICO_SEL_AUTO = the shape rule)
+int pico_sel(int knob);
 // true when kernel id `kid` is being timed: *start / *stop are the next free event pair of its pool
 bool pico_prof_events(int kid, hipEvent_t* start, hipEvent_t* stop);
 

@@ -203,13 +203,10 @@ constexpr int PREV_COLS = 16;  // column slots per workgroup (cpw <= 16)
 // dw partial per workgroup (deterministic two-stage reduction, no atomics).
 // FULL: cols == MAXC * 512 (every lane chunk in range: no per-chunk predicates, which otherwise
 // make hipcc spill). NW waves per workgroup (16 up to 1024 columns, 8 up to 2048, 4 above — the
-// most that fit without spilling), R rows per wave per pass (every load of the R rows in flight before
-// the first use; R = 2 measured 13.33 vs 13.06 us for R = 1 on the SmolLM chained launch, so 1 by default),
-// at most one workgroup per CU; the per-wave dw partials accumulate in LDS and the workgroup's sum is one
-// fp32 row per CU. The weight chunks are loaded once per wave (loop-invariant).
-#ifndef PICO_RMS_BWD_R
-#define PICO_RMS_BWD_R 1
-#endif
+// most that fit without spilling), one row per wave per pass, at most one workgroup per CU; the per-wave dw
+// partials accumulate in LDS and the workgroup's sum is one fp32 row per CU. The weight chunks are loaded once
+// per wave (loop-invariant). (Measured and removed: two rows per wave per pass, 16.0 -> 16.7 us in the step;
+// 16 waves at 2048 columns, 15.3 -> 42.8 us.)
 template <int MAXC, int NW, bool FULL, bool RES>
 __global__ __launch_bounds__(NW * 64) void rmsnorm_bwd_kernel(const bf16_t* __restrict__ dy,
                                                               const bf16_t* __restrict__ dres,
@@ -217,8 +214,6 @@ __global__ __launch_bounds__(NW * 64) void rmsnorm_bwd_kernel(const bf16_t* __re
                                                               const float* __restrict__ rstd, bf16_t* __restrict__ dx,
                                                               float* __restrict__ dw_part, int64_t rows, int cols,
                                                               const DwPrev prev) {
-  // R rows only where they fit without spilling (16-wave MAXC 2 and the predicated MAXC 4 forms do not)
-  constexpr int R = (MAXC == 1 || MAXC == 8 || (MAXC == 4 && FULL)) ? PICO_RMS_BWD_R : 1;
   __shared__ float red[NW * MAXC * 512];  // per-wave dw partial rows (accumulated in LDS, not registers)
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
@@ -250,61 +245,49 @@ __global__ __launch_bounds__(NW * 64) void rmsnorm_bwd_kernel(const bf16_t* __re
     if (FULL || (c * 64 + lane) * 8 < cols) wv[c] = *reinterpret_cast<const u16x8*>(w + lane * 8 + 512 * c);
   const int64_t stride = (int64_t)gridDim.x * NW;
 #pragma unroll 1
-  for (int64_t row0 = (int64_t)blockIdx.x * NW + wid; row0 < rows; row0 += R * stride) {
-    u16x8 xv[R][MAXC], dv[R][MAXC], rv[R][MAXC];
-    float rs[R];
+  for (int64_t row = (int64_t)blockIdx.x * NW + wid; row < rows; row += stride) {
+    u16x8 xv[MAXC], dv[MAXC], rv[MAXC];
+    const float rs = rstd[row];
+    const int64_t ro = row * cols + lane * 8;  // this lane's first element of the row; chunk c at + 512 c
 #pragma unroll
-    for (int r = 0; r < R; ++r) {  // every load of the R rows in flight before any use
-      const int64_t row = row0 + r * stride;
-      if (r == 0 || row < rows) {  // wave-uniform
-        rs[r] = rstd[row];
-        const int64_t ro = row * cols + lane * 8;  // this lane's first element of the row; chunk c at + 512 c
-#pragma unroll
-        for (int c = 0; c < MAXC; ++c) {
-          if (FULL || (c * 64 + lane) * 8 < cols) {
-            xv[r][c] = *reinterpret_cast<const u16x8*>(x + ro + 512 * c);
-            dv[r][c] = *reinterpret_cast<const u16x8*>(dy + ro + 512 * c);
-            if constexpr (RES) rv[r][c] = *reinterpret_cast<const u16x8*>(dres + ro + 512 * c);
-          }
-        }
+    for (int c = 0; c < MAXC; ++c) {
+      if (FULL || (c * 64 + lane) * 8 < cols) {
+        xv[c] = *reinterpret_cast<const u16x8*>(x + ro + 512 * c);
+        dv[c] = *reinterpret_cast<const u16x8*>(dy + ro + 512 * c);
+        if constexpr (RES) rv[c] = *reinterpret_cast<const u16x8*>(dres + ro + 512 * c);
       }
     }
+    float dot = 0.f;
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const int64_t row = row0 + r * stride;
-      if (r > 0 && row >= rows) break;  // wave-uniform
-      float dot = 0.f;
+    for (int c = 0; c < MAXC; ++c) {
+      if (FULL || (c * 64 + lane) * 8 < cols) {
+        f32x4 a = *reinterpret_cast<const f32x4*>(myred + 512 * c);
+        f32x4 bq = *reinterpret_cast<const f32x4*>(myred + 512 * c + 4);
 #pragma unroll
-      for (int c = 0; c < MAXC; ++c) {
-        if (FULL || (c * 64 + lane) * 8 < cols) {
-          f32x4 a = *reinterpret_cast<const f32x4*>(myred + 512 * c);
-          f32x4 bq = *reinterpret_cast<const f32x4*>(myred + 512 * c + 4);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const float xh = bf2f(xv[r][c][j]) * rs[r], d = bf2f(dv[r][c][j]);
-            if (j < 4) a[j] += d * xh;
-            else bq[j - 4] += d * xh;
-            dot += d * bf2f(wv[c][j]) * xh;
-          }
-          *reinterpret_cast<f32x4*>(myred + 512 * c) = a;
-          *reinterpret_cast<f32x4*>(myred + 512 * c + 4) = bq;
+        for (int j = 0; j < 8; ++j) {
+          const float xh = bf2f(xv[c][j]) * rs, d = bf2f(dv[c][j]);
+          if (j < 4) a[j] += d * xh;
+          else bq[j - 4] += d * xh;
+          dot += d * bf2f(wv[c][j]) * xh;
         }
+        *reinterpret_cast<f32x4*>(myred + 512 * c) = a;
+        *reinterpret_cast<f32x4*>(myred + 512 * c + 4) = bq;
       }
-      dot = wave_sum(dot) / (float)cols;
-      bf16_t* dxr = dx + row * cols + lane * 8;
+    }
+    dot = wave_sum(dot) / (float)cols;
+    bf16_t* dxr = dx + ro;
 #pragma unroll
-      for (int c = 0; c < MAXC; ++c) {
-        if (FULL || (c * 64 + lane) * 8 < cols) {
-          u16x8 o;
+    for (int c = 0; c < MAXC; ++c) {
+      if (FULL || (c * 64 + lane) * 8 < cols) {
+        u16x8 o;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const float xh = bf2f(xv[r][c][j]) * rs[r];
-            float v = rs[r] * (bf2f(dv[r][c][j]) * bf2f(wv[c][j]) - xh * dot);
-            if constexpr (RES) v += bf2f(rv[r][c][j]);
-            o[j] = f2bf(v);
-          }
-          *reinterpret_cast<u16x8*>(dxr + 512 * c) = o;
+        for (int j = 0; j < 8; ++j) {
+          const float xh = bf2f(xv[c][j]) * rs;
+          float v = rs * (bf2f(dv[c][j]) * bf2f(wv[c][j]) - xh * dot);
+          if constexpr (RES) v += bf2f(rv[c][j]);
+          o[j] = f2bf(v);
         }
+        *reinterpret_cast<u16x8*>(dxr + 512 * c) = o;
       }
     }
   }
@@ -342,10 +325,7 @@ __global__ __launch_bounds__(NW * 64) void rmsnorm_bwd_kernel(const bf16_t* __re
   }
 }
 
-#ifndef PICO_RMS_BWD_NW4
-#define PICO_RMS_BWD_NW4 8
-#endif
-constexpr int bwd_waves(int maxc) { return maxc <= 2 ? 16 : (maxc == 4 ? PICO_RMS_BWD_NW4 : 4); }
+constexpr int bwd_waves(int maxc) { return maxc <= 2 ? 16 : (maxc == 4 ? 8 : 4); }
 
 template <int M>
 int launch_rmsnorm_bwd(const void* dy, const void* dres, const void* x, const void* w, const float* rstd, void* dx,

@@ -11,6 +11,8 @@
 #include <vector>
 #include "common.h"
 
+#include <cstdlib>
+
 static thread_local char g_err[512] = "";
 
 int pico_set_error(const char* fmt, ...) {
@@ -58,9 +60,39 @@ bool pico_prof_events(int kid, hipEvent_t* start, hipEvent_t* stop) {
   return true;
 }
 
+namespace {
+// knob values: the environment once, at first use (_lib.load() calls pico_select when it loads the library), then
+// pico_select
+struct SelTable {
+  int v[PICO_SEL_COUNT];
+  SelTable() {
+    static const char* const names[PICO_SEL_COUNT] = {"PICO_ATTN_KVP", "PICO_KVP_WAVES", "PICO_ATTN_GROUPS",
+                                                      "PICO_ATTN_FWD"};
+    for (int i = 0; i < PICO_SEL_COUNT; ++i) {
+      const char* e = getenv(names[i]);
+      v[i] = (e && *e) ? atoi(e) : PICO_SEL_AUTO;
+    }
+  }
+};
+SelTable& sel_table() {
+  static SelTable t;
+  return t;
+}
+}  // namespace
+
+int pico_sel(int knob) { return (knob >= 0 && knob < PICO_SEL_COUNT) ? sel_table().v[knob] : PICO_SEL_AUTO; }
+
+
 extern "C" {
 
 int pico_abi_version(void) { return PICO_ABI_VERSION; }
+
+int pico_select(int knob, int value) {
+  if (knob < 0 || knob >= PICO_SEL_COUNT) return -2;
+  const int old = sel_table().v[knob];
+  sel_table().v[knob] = value;
+  return old;
+}
 
 const char* pico_last_error(void) { return g_err; }
 

@@ -110,9 +110,13 @@ class DataParallelBucket(nn.Module):
     def comm_report(self):
         """Per recorded syncing backward (after a device synchronize): {"exposed_ms": end of backward -> end of
         the post-backward wait, "buckets": [(ready_ms, allreduce_done_ms, bytes)] relative to the end of the
-        backward (negative: before it), in bucket order}."""
+        backward (negative: before it), in bucket order}.
+        A pass recorded without an anchor (timing switched on partway through it) is skipped; a bucket that did not
+        sync in a pass reports (None, None, bytes)."""
         out = []
         for a, t0, t1, bk in self._comm_log or []:
+            if a is None or t0 is None or t1 is None:
+                continue
             end = a.elapsed_time(t0)  # every time from the anchor (elapsed times are taken forward only)
             rows = [(a.elapsed_time(tm[0]) - end, a.elapsed_time(tm[1]) - end, nb) if tm is not None else
                     (None, None, nb) for tm, nb in bk]

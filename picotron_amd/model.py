@@ -22,7 +22,6 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from . import layer_order
 from . import ops
 from . import wgrad_pair as WP
 from . import process_group_manager as pgm
@@ -375,11 +374,9 @@ class Llama(nn.Module):
         delta, residual = x, None
         down = None  # the previous layer's down-projection pair hint (wgrad_pair)
         for b, layer in enumerate(self.decoder_layers):
-            delta, residual = layer_order.boundary(delta, residual, b)  # identity (pipelined graph: bwd order)
             delta, residual = layer.forward_fused(delta, residual, prev_down=down)
             hints = layer._pair_hints()
             down = hints["down"] if hints else None
-        delta, residual = layer_order.boundary(delta, residual, len(self.decoder_layers))
         # the fused LM head + CE (return_hidden) groups its weight gradient too: the final norm's y^T goes into the
         # head's x^T group slot (wgrad_pair)
         head = getattr(self, "final_proj", None)

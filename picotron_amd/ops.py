@@ -889,8 +889,9 @@ class _LMHeadCEChunkedFn(torch.autograd.Function):
         from . import wgrad_pair as WP
         grouped = (need_w and chunk >= T and kind in ("main", "grad") and WP.active()
                    and os.getenv("PICO_LM_WGRAD_GROUP", "1") != "0")
-        if grouped:
-            buf = WP.dy_out(w, V, H, T, x.dtype, x.device)
+        if grouped:  # only when the final norm put this micro-batch's x^T into the head's group slot:
+            # otherwise plan() runs a GEMM per micro-batch and a [G T, V] group buffer would be dead weight
+            buf = WP.dy_out_if_paired(w, xin, V, H, T, x.dtype, x.device)
         if buf is None:
             buf = torch.empty(chunk, V, dtype=x.dtype, device=x.device)
         for c0 in range(0, T, chunk):

@@ -8,7 +8,6 @@ import time
 import torch
 import torch.nn.functional as F
 
-from . import layer_order as LO
 from . import process_group_manager as pgm
 from . import wgrad_pair as WP
 
@@ -39,11 +38,6 @@ def _fused_lm_head(model):
     if not w.is_cuda or w.dtype != torch.bfloat16 or w.shape[0] % 8 != 0:
         return None
     return head
-
-
-def _layer_ordered():
-    """PICO_LAYER_ORDER=1: the pipelined graph orders its backwards per layer (layer_order) instead of whole."""
-    return os.getenv("PICO_LAYER_ORDER", "0") == "1"
 
 
 def _forward_loss(model, input_ids, target_ids, grad_acc_steps, loss_acc=None):
@@ -249,14 +243,13 @@ class PipelinedMicroBatchGraph:
         k = inp.shape[0]
         losses = [None] * k
         bwd_done = fwd_done = None
-        # layer-ordered backwards (layer_order): backward i enters each layer after backward i - 1 has left it,
-        # instead of starting after backward i - 1 has ended
-        sched = LO.Schedule() if _layer_ordered() else None
+        # (layer-ordered backwards -- backward i entering each layer after backward i - 1 left it -- measured
+        # bit-identical and step-neutral in round 5, and removed)
         for i in range(k + 1):
             if i >= 1:  # backward of micro-batch i - 1 (on its forward's stream), after backward i - 2
                 st = streams[(i - 1) % 2]
                 with torch.cuda.stream(st), ops.no_side_streams(), WP.micro_batch(i - 1, n):
-                    if bwd_done is not None and sched is None:
+                    if bwd_done is not None:
                         st.wait_event(bwd_done)
                     loss, folded = losses[i - 1]
                     loss.backward()
@@ -264,13 +257,10 @@ class PipelinedMicroBatchGraph:
                         acc += loss.detach()
                     bwd_done = torch.cuda.Event()
                     bwd_done.record(st)
-                    if sched is not None:
-                        sched.backward_done(i - 1, bwd_done)
                 losses[i - 1] = None
             if i < k:  # forward of micro-batch i, after forward i - 1
                 st = streams[i % 2]
-                with torch.cuda.stream(st), ops.no_side_streams(), WP.micro_batch(i, n), (
-                        sched.forward(i) if sched is not None else contextlib.nullcontext()):
+                with torch.cuda.stream(st), ops.no_side_streams(), WP.micro_batch(i, n):
                     if fwd_done is not None:
                         st.wait_event(fwd_done)
                     losses[i] = _forward_loss(model, inp[i], tgt[i], n, acc)

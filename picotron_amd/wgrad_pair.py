@@ -157,8 +157,8 @@ def dy_out_existing(weight, N, K, T, dtype, device):
 
 def footprint_bytes():
     """Bytes held by every live pair buffer: per projection (weight [N, K], T tokens per micro-batch, G per group)
-    two x^T sets [K, G T] and one dy [G T, N] — G (2 K T + T N) elements; SmolLM-1.7B at T = 4096, G = 2: about
-    0.9 GB per layer."""
+    two x^T sets [K, G T] and one dy [G T, N] — G (2 K T + T N) elements; SmolLM-1.7B at T = 4096, G = 4: about
+    1.8 GB per layer, plus the LM head's when its x^T is grouped (dy [4T, V]: 1.6 GB). bench.py reports it."""
     return sum(sum(x.numel() * x.element_size() for x in b.xt) + b.dy.numel() * b.dy.element_size()
                for _, b in list(_BUFS.values()))
 

@@ -5,6 +5,7 @@ issues, not when it completes). Prints the mean cycles per 64-row tile and phase
 dispatch class (block group g -> g * nbh / CUs: oldest first). The stamps cost ~10 % themselves.
 
   PICO_LIB_PATH=picotron_amd/lib/variants/kvpstamp.so PICO_ATTN_KVP=1 python scripts/kvp_stamps.py
+(PICO_KVP_WAVES=8 for the 8-wave workgroups: the stamps are 16 words per wave at (block * NW + wave) * 16.)
 """
 import ctypes
 import json
@@ -41,7 +42,8 @@ def main():
         ws[nbytes - 65536 * 4 * 8:].zero_()
         L.check(lib.pico_attn_bwd(ctypes.byref(a), L.stream_of(q)), "bwd")
     torch.cuda.synchronize()
-    st = ws[nbytes - 65536 * 4 * 8:].cpu().numpy().view(np.uint64).astype(np.float64).reshape(-1, 4, 16)
+    nw = 8 if os.environ.get("PICO_KVP_WAVES") == "8" else 4  # waves per workgroup of the launch
+    st = ws[nbytes - 65536 * 4 * 8:].cpu().numpy().view(np.uint64).astype(np.float64).reshape(-1, nw, 16)
     live = st[:, 0, 7] > 0
     st = st[live]
     nwg = st.shape[0]

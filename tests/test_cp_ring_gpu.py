@@ -53,7 +53,7 @@ def _staged_comm_class(base):
     return HostStagedCommunicate
 
 
-def _worker(rank, world, port, causal, zigzag=False, S=1024):
+def _worker(rank, world, port, causal, zigzag=False, S=1024, B=2, Hq=4, rope=False):
     import sys
     sys.path.insert(0, ROOT)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -68,21 +68,32 @@ def _worker(rank, world, port, causal, zigzag=False, S=1024):
     CP.ContextCommunicate = _staged_comm_class(CP.ContextCommunicate)
 
     dev = "cuda:0"
-    B, Hq, D = 2, 4, 64
+    D = 64
     g = torch.Generator(device="cpu").manual_seed(21)  # identical full tensors on every rank
     q, k, v, do = [torch.randn(B, S, Hq, D, generator=g).to(BF).to(dev) for _ in range(4)]
     scale = D ** -0.5
+    # rope: q and k rotated before attention with the whole-sequence tables, and on each rank with the tables
+    # update_rope_for_context_parallel slices for it (ref picotron/context_parallel/context_parallel.py:189-195,
+    # ref picotron/model.py:135-136) — at C5 that is positions up to 32,767
+    if rope:
+        from picotron_amd.model import get_cos_sin
+        cos, sin = get_cos_sin(S, D, base=10000.0)
+        cos, sin = cos.to(dev), sin.to(dev)
+        cosl, sinl = CP.update_rope_for_context_parallel(cos, sin)
+        rot = lambda x, c, s_: ops.apply_rotary_emb(x, c[:, : D // 2], s_[:, : D // 2])  # noqa: E731
     # whole-sequence reference through the same kernels (pinned to the fp64 oracle by test_kernels_gpu)
     qf, kf, vf = [t.clone().requires_grad_(True) for t in (q, k, v)]
-    of = ops.flash_attn_func(qf, kf, vf, softmax_scale=scale, causal=causal)
+    qa, ka = (rot(qf, cos, sin), rot(kf, cos, sin)) if rope else (qf, kf)
+    of = ops.flash_attn_func(qa, ka, vf, softmax_scale=scale, causal=causal)
     of.backward(do)
     n = S // world
     # this rank's rows: contiguous chunk (reference split) or the zig-zag pair of chunks
     sl = CP.zigzag_positions(S, rank, world).to(dev) if zigzag else slice(rank * n, (rank + 1) * n)
     ql, kl, vl = [t[:, sl].contiguous().requires_grad_(True) for t in (q, k, v)]
+    qla, kla = (rot(ql, cosl, sinl), rot(kl, cosl, sinl)) if rope else (ql, kl)
     # exactly the reference's call (ref picotron/model.py:139-150): [B, S, H, D] projections transposed to
     # [B, H, S, D], ring_attention, output transposed back to [B, S, H, D]
-    ol = CP.ring_attention(ql.transpose(1, 2), kl.transpose(1, 2), vl.transpose(1, 2), scale, causal).transpose(1, 2)
+    ol = CP.ring_attention(qla.transpose(1, 2), kla.transpose(1, 2), vl.transpose(1, 2), scale, causal).transpose(1, 2)
     assert ol.shape == ql.shape
     ol.backward(do[:, sl].contiguous())
     torch.cuda.synchronize()
@@ -102,14 +113,17 @@ def _worker(rank, world, port, causal, zigzag=False, S=1024):
         raise AssertionError(f"rank {rank} cp={world} causal={causal} zigzag={zigzag}: {bad} (all: {errs})")
 
 
-@pytest.mark.parametrize("world,causal,zigzag,S", [(2, True, False, 1024), (4, True, False, 1024),
-                                                   (2, False, False, 1024), (2, True, True, 1024),
-                                                   (4, True, True, 1024), (8, True, False, 2048),
-                                                   (8, True, True, 2048)])
-def test_ring_attention_multi_rank(world, causal, zigzag, S):
+@pytest.mark.parametrize("world,causal,zigzag,S,B,Hq,rope", [
+    (2, True, False, 1024, 2, 4, False), (4, True, False, 1024, 2, 4, False), (2, False, False, 1024, 2, 4, False),
+    (2, True, True, 1024, 2, 4, False), (4, True, True, 1024, 2, 4, True), (8, True, False, 2048, 2, 4, False),
+    (8, True, True, 2048, 2, 4, False),
+    # config 5 itself (BASELINE configs[4]): cp = 8 at S = 32768, S_local = 4096 — the last rank's eight-block chain of
+    # 4096-row blocks and the RoPE tables sliced per rank at positions up to 32,767; B = 1, 2 heads
+    (8, True, False, 32768, 1, 2, True), (8, True, True, 32768, 1, 2, True)])
+def test_ring_attention_multi_rank(world, causal, zigzag, S, B, Hq, rope):
     """Contiguous (reference) split, and the zig-zag split (PICO_CP_ZIGZAG=1: rank r holds chunks r and
     2 cp - 1 - r; every rank does equal block work), against whole-sequence attention at the rows each
     rank holds. cp = 8 (C5's ring size): the 8-step ring loop, and the zig-zag split
-    into 2 cp = 16 chunks, at S = 2048."""
-    mp.start_processes(_worker, args=(world, _free_port(), causal, zigzag, S), nprocs=world, join=True,
+    into 2 cp = 16 chunks, at S = 2048 and at C5's own S = 32768."""
+    mp.start_processes(_worker, args=(world, _free_port(), causal, zigzag, S, B, Hq, rope), nprocs=world, join=True,
                        start_method="spawn")

@@ -427,7 +427,7 @@ def test_attention_bwd_d128_key_block_groups(S, Hq, Hkv, causal, mode):
 ])
 def test_attention_bwd_d64_kv_kernels(monkeypatch, B, Sq, Sk, Hq, Hkv, causal, mode):
     """D = 64 dK/dV: attn_bwd_kvp_kernel (64-row query tiles, 4 or 8 waves x 32 keys per workgroup: the default up
-    to 4096 keys) and the 32-row attn_bwd_kv_kernel (PICO_ATTN_KVP=0 / 1 and PICO_KVP_WAVES=4 / 8 force each), each
+    to 4096 keys) and the 32-row attn_bwd_kv_kernel (pico_select PICO_SEL_ATTN_KVP / PICO_SEL_KVP_WAVES force each), each
     with its matching dQ-kernel LSE form, vs an fp32 torch reference, and within bf16 rounding of each other."""
     from picotron_amd.model import get_cos_sin
     ops = _ops()
@@ -455,9 +455,10 @@ def test_attention_bwd_d64_kv_kernels(monkeypatch, B, Sq, Sk, Hq, Hkv, causal, m
         ops._rope_launch(gk.to(BF).contiguous(), rk, cos, sin, True)
         gq, gk = rq.float(), rk.float()
     res = {}
+    from picotron_amd import _lib as L
     for kvp in ("0", "1", "1w8"):
-        monkeypatch.setenv("PICO_ATTN_KVP", kvp[0])
-        monkeypatch.setenv("PICO_KVP_WAVES", "8" if kvp.endswith("w8") else "4")
+        L.select(L.SEL_ATTN_KVP, int(kvp[0]))
+        L.select(L.SEL_KVP_WAVES, 8 if kvp.endswith("w8") else 4)
         if mode == "bf16":
             dq, dk, dv = ops.attention_block_bwd(do, q, k, v, o, lse, sc, causal)
         elif mode == "f32acc":
@@ -468,6 +469,8 @@ def test_attention_bwd_d64_kv_kernels(monkeypatch, B, Sq, Sk, Hq, Hkv, causal, m
             dq, dk, dv = [torch.empty_like(t) for t in (q, k, v)]
             ops._attention_bwd_into(do, q, k, v, o, lse, sc, causal, dq, dk, dv, rope=(cos, sin))
         torch.cuda.synchronize()
+        L.select(L.SEL_ATTN_KVP, L.SEL_AUTO)
+        L.select(L.SEL_KVP_WAVES, L.SEL_AUTO)
         res[kvp] = [t.float() for t in (dq, dk, dv)]
         for a, b in zip(res[kvp], (gq, gk, gv)):
             assert rel_l2(a, b) < 1e-2, (kvp, rel_l2(a, b))
