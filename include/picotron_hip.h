@@ -96,7 +96,7 @@ enum {
   PICO_SEL_ATTN_KVP = 0,    /* PICO_ATTN_KVP: D=64 dK/dV kernel, 1 = 64-row attn_bwd_kvp_kernel, 0 = 32-row kernel */
   PICO_SEL_KVP_WAVES = 1,   /* PICO_KVP_WAVES: waves per attn_bwd_kvp_kernel workgroup, 4 or 8 */
   PICO_SEL_ATTN_GROUPS = 2, /* PICO_ATTN_GROUPS: one-round block groups of the causal dK/dV grid, 1 on / 0 off */
-  PICO_SEL_ATTN_FWD = 3,    /* PICO_ATTN_FWD: forward kernel, 1 = persistent 64-row-per-wave kernel, 0 = 32-row */
+  PICO_SEL_ATTN_FWD = 3,    /* PICO_ATTN_FWD: 1 = the persistent 64-row-per-wave forward (opt-in, measured slower) */
   PICO_SEL_COUNT = 4
 };
 int pico_select(int knob, int value);

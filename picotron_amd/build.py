@@ -30,6 +30,7 @@ CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno
 FILE_FLAGS = {
     "attn_bwd_split.hip": ["-fno-slp-vectorize", "-mllvm", "-amdgpu-mfma-vgpr-form"],
     "attn_fwd.hip": ["-fno-slp-vectorize", "-fno-honor-nans"],
+    "attn_fwdp.hip": ["-fno-slp-vectorize", "-fno-honor-nans", "-mllvm", "-amdgpu-mfma-vgpr-form"],
     "attn_bwd_split_d128.hip": ["-fno-slp-vectorize"],
 }
 

@@ -493,6 +493,7 @@ int launch_fwd(const pico_attn_args* a, hipStream_t s) {
 }  // namespace
 
 int pico_attn_check_common(const pico_attn_args* a, const char* op);
+int pico_attn_fwdp(const pico_attn_args* a, hipStream_t s);
 extern "C" int pico_attn_fwd(const pico_attn_args* a, void* stream) {
   int rc = pico_attn_check_common(a, "pico_attn_fwd");
   if (rc) return rc;
@@ -509,6 +510,8 @@ extern "C" int pico_attn_fwd(const pico_attn_args* a, void* stream) {
   }
   if (a->batch == 0 || a->seqlen_q == 0 || a->heads_q == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
+  const int rp = pico_attn_fwdp(a, s);  // the persistent 64-row-per-wave kernel where it applies (attn_fwdp.hip)
+  if (rp >= 0) return rp;
   if (a->head_dim == 64) return launch_fwd<64>(a, s);
   return launch_fwd<128>(a, s);
 }
