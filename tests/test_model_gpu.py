@@ -626,9 +626,9 @@ def test_bench_dp2_gloo_on_one_gpu():
     assert math.isfinite(out["loss_last"]) and out["loss_last"] < math.log(49152) + 0.1
     ar = out["allreduce"]
     assert ar["buckets"] > 0 and ar["bytes"] > 0 and ar["busbw_GBps"] > 0
-    # the step's exposed all-reduce: measured per timed step, plus the W = 8 model
-    assert ar["exposed_ms"] >= 0 and len(ar["bucket_ready_ms"]) == ar["buckets"]
-    assert set(ar["model_exposed_ms"]) == {"300.0", "600.0", "1071.0"}
+    # the step's exposed all-reduce is measured on RCCL only (gloo's Work.wait() blocks the host inside the
+    # backward): reported as not measured here; test_bench_dp_bucket_grad_acc1_rccl covers the RCCL form
+    assert ar["exposed_ms"] is None and "gloo" in ar["exposed_over"]
 
 
 def test_bench_dp_bucket_grad_acc1_rccl():
@@ -647,7 +647,9 @@ def test_bench_dp_bucket_grad_acc1_rccl():
     out = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
     assert math.isfinite(out["loss_last"]) and out["config"]["grad_acc"] == 1
     ar = out["allreduce"]
+    # measured over the untimed step(s) after the throughput region (bench --comm-steps), plus the W = 8 model
     assert ar["exposed_ms"] >= 0 and ar["buckets"] == len(ar["bucket_bytes"])
+    assert set(ar["model_exposed_ms"]) == {"300.0", "600.0", "1071.0"}
 
 
 def test_smollm_step_pipelined_paired_matches_eager(monkeypatch):
