@@ -917,7 +917,8 @@ def test_attention_rope_q_fwd_fused(B, S, Hq, Hkv, D, causal):
     assert torch.equal(q.cpu(), H.rope_fused(q_unrot.cpu(), cos.cpu(), sin.cpu()))
 
 
-@pytest.mark.parametrize("B,S,H,D,causal", [(2, 256, 4, 64, True), (1, 200, 2, 128, False)])
+@pytest.mark.parametrize("B,S,H,D,causal", [(2, 256, 4, 64, True), (1, 200, 2, 128, False), (4, 1024, 32, 64, True),
+                                             (1, 100, 2, 64, True), (3, 140, 2, 128, True)])
 def test_attention_fwd_transposed_output(B, S, H, D, causal):
     """pico_attn_fwd's optional o_t output == O transposed to [H*D, tokens], bit for bit (same rounding),
     and O itself unchanged by requesting it."""
