@@ -390,3 +390,19 @@ def test_train_step_announces_micro_batches():
             del os.environ["PICO_WGRAD_PAIR"]
         else:
             os.environ["PICO_WGRAD_PAIR"] = old
+
+
+def test_kernel_selection_knobs(lib):
+    """pico_select (include/picotron_hip.h): every knob starts at its environment value or PICO_SEL_AUTO, is set
+    and restored through the ABI (returning the previous value), and an unknown knob is rejected — no launch reads
+    the process environment. CPU only: selection touches no device."""
+    from picotron_amd import _lib
+    for knob in (_lib.SEL_ATTN_KVP, _lib.SEL_KVP_WAVES, _lib.SEL_ATTN_GROUPS, _lib.SEL_ATTN_FWD):
+        env = os.environ.get(("PICO_ATTN_KVP", "PICO_KVP_WAVES", "PICO_ATTN_GROUPS", "PICO_ATTN_FWD")[knob])
+        start = _lib.select(knob, 1)
+        assert start == (int(env) if env else _lib.SEL_AUTO)
+        assert _lib.select(knob, 0) == 1
+        assert _lib.select(knob, start) == 0
+    assert lib.pico_select(99, 0) == -2 and lib.pico_select(-1, 0) == -2
+    with pytest.raises(ValueError):
+        _lib.select(99, 0)
