@@ -361,7 +361,14 @@ __global__ __launch_bounds__(256, QCfg<D>::MINB) void attn_bwd_q_kernel(const pi
       const int t = t0 + u;
       if (t >= ntiles) break;
       if (t > 0) {  // tile t landed (this wave's pieces); the younger tiles stay in flight
-        wait_vmcnt(min(P - 1, ntiles - 1 - t) * C::NPW);  // issued tiles after t stay in flight
+        if constexpr (P == 2) {  // counts as immediates (a runtime wait_vmcnt(n) is a compare-and-branch chain)
+          if (t + 1 < ntiles) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::NPW) : "memory");
+          else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else if constexpr (P == 1) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else {
+          wait_vmcnt(min(P - 1, ntiles - 1 - t) * C::NPW);  // issued tiles after t stay in flight
+        }
       }
       lds_barrier();  // every wave's pieces of tile t visible; slot (t + P) % NBUF no longer read
       const int n0 = t * KT;
@@ -1087,9 +1094,19 @@ __global__ __launch_bounds__(NW * 64, MINB) void attn_bwd_kvp_kernel(const pico_
       ph[7] += 1;
 #endif
       if (t > 0) {
-        // this wave's pieces of tile t landed; those of the younger tiles already issued stay in flight
-        const int younger = min(C::PD - 1, ntiles - 1 - t);
-        wait_vmcnt(younger * (wave == 0 ? PPW + 1 : PPW));
+        // this wave's pieces of tile t landed; those of the younger tiles already issued stay in flight (counts as
+        // immediates: a runtime wait_vmcnt(n) compiles to a compare-and-branch chain, ~12 branches per tile)
+        if constexpr (C::PD == 2) {
+          if (t + 1 < ntiles) {
+            if (wave == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW + 1) : "memory");
+            else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");
+          } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          }
+        } else {
+          const int younger = min(C::PD - 1, ntiles - 1 - t);
+          wait_vmcnt(younger * (wave == 0 ? PPW + 1 : PPW));
+        }
         KVP_ST(0);
         lds_barrier();  // every wave's pieces of tile t visible; the slot of tile t - 1 is no longer read
         KVP_ST(1);
