@@ -31,7 +31,7 @@ FILE_FLAGS = {
     "attn_bwd_split.hip": ["-fno-slp-vectorize", "-mllvm", "-amdgpu-mfma-vgpr-form"],
     "attn_fwd.hip": ["-fno-slp-vectorize", "-fno-honor-nans"],
     "attn_fwdp.hip": ["-fno-slp-vectorize", "-fno-honor-nans", "-mllvm", "-amdgpu-mfma-vgpr-form"],
-    "attn_bwd_split_d128.hip": ["-fno-slp-vectorize"],
+    "attn_bwd_split_d128.hip": ["-fno-slp-vectorize", "-mllvm", "-amdgpu-mfma-vgpr-form"],
 }
 
 

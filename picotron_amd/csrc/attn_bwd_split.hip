@@ -1374,6 +1374,435 @@ int kvp_waves(const pico_attn_args* a) {
 }
 #endif  // !PICO_SPLIT_D128_TU
 
+#ifdef PICO_SPLIT_D128_TU
+// ------------------------------------------------------------------------------------------------
+// dK / dV kernel, D = 128, 64-row query tiles in a slot-ordered stream (round 6)
+// ------------------------------------------------------------------------------------------------
+// attn_bwd_kvp_kernel's form carried to head_dim 128: a workgroup = 4 waves x 32 keys (dK / dV of the wave's keys
+// in 128 accumulator registers, K / V fragments resident), each ring tile 64 query rows as halves A / B whose
+// phases interleave inside the wave:
+//     M1(A) | A's then B's Q / dO operands,  M1(B) | V(A) + A's transposed reads,  M2(A) | V(B) + B's reads,
+//     M2(B) | the DMA of tile t + 2
+// 16 MFMAs per phase (64 per tile: at D = 128 the tile is MFMA-bound, ~130 VALU against 2,048 matrix cycles), one
+// wave per SIMD (the whole register file; one 99-KiB workgroup per CU). The 32-row kernel it replaces runs each
+// 32-row tile as one dependency chain (S / dP -> softmax -> dV / dK) at one wave per SIMD: 0.22 MFMA busy at C4.
+// Operands are read two slots ahead of their MFMA; the schedule is fenced per slot (sched_barrier).
+constexpr int QT2 = 64;  // query rows per ring tile (the D = 64 TU defines it with attn_bwd_kvp_kernel)
+struct KV2Cfg {
+  static constexpr int D = 128, KS = 8, DT = 4;
+  static constexpr int QIMG = QT2 * 256;         // one Q (or dO) 64-row image (kv2_off), 16 KiB
+  static constexpr int LSD = 1024;               // -LSE/scale [64] | -delta [64] (+ 512 B the DMA piece repeats)
+  static constexpr int SLOT = 2 * QIMG + LSD;    // 33 KiB
+  static constexpr int NBUF = 3, PD = NBUF - 1;  // 99 KiB per workgroup, prefetch distance 2
+  static constexpr int NQP = QIMG / 1024;        // 16 pieces per image
+  static constexpr int PPW = 2 * NQP / 4;        // 8 image pieces per wave per tile (+ wave 0's LSE / delta piece)
+};
+
+#define KV2_SLOT() __builtin_amdgcn_sched_barrier(0)
+
+// byte offset of 16-byte chunk ch (0..15) of row `row` in a [64][128 x bf16] image of 8-row x 32-column subtiles of
+// 512 B (cdna_hip_programming.md T11 image (a)): the row reads of a k-step parity and the transposed reads of a row
+// parity share one base register each (every other offset an immediate), both conflict-free
+PICO_DEV int kv2_off(int row, int ch) {
+  return 2048 * (row >> 3) + 512 * (ch >> 2) + 64 * (row & 7) + 16 * ((ch & 3) ^ ((row >> 2) & 3));
+}
+
+template <bool CAUSAL>
+__global__ __launch_bounds__(256, 1) void attn_bwd_kvp128_kernel(const pico_attn_args a, float scale, float c2,
+                                                                 const float* __restrict__ sinit_g,
+                                                                 const float* __restrict__ delta_g, int sq_pad,
+                                                                 int hsplit, float* __restrict__ dkv_part,
+                                                                 const BlkGroups grp,
+                                                                 unsigned long long* __restrict__ stamp_out) {
+  using C = KV2Cfg;
+#if PICO_KVP_STAMP  // the stamp words of attn_bwd_kvp_kernel (scripts/kvp_stamps.py): 0 wait, 1 barrier, 3-6 phases
+  unsigned long long ph[16] = {0}, tlast = 0, tblk = 0;
+  ph[10] = __builtin_amdgcn_s_memrealtime();
+  ph[12] = __builtin_amdgcn_s_memtime();
+#define KV2_ST(i)                                               \
+  {                                                             \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+    ph[i] += t_ - tlast;                                        \
+    tlast = t_;                                                 \
+  }
+#else
+#define KV2_ST(i)
+#endif
+  constexpr int KS = C::KS, DT = C::DT, PPW = C::PPW, NW = 4, KB = 32 * NW;
+  static_assert(PPW == 8 && 2 * C::NQP == PPW * NW, "8 image pieces per wave: the odd slots of M2(B)");
+  __shared__ __attribute__((aligned(16))) char smem[C::NBUF * C::SLOT];
+
+  const int lane0 = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int Sq = (int)a.seqlen_q, Sk = (int)a.seqlen_k;
+  const int Hq = (int)a.heads_q;
+  const int G = (int)(a.heads_q / a.heads_kv);
+  const int nbh = (int)(a.batch * a.heads_kv) * hsplit;
+  const int gi = blockIdx.x / nbh;
+  const int bhs = blockIdx.x % nbh;
+  const int hs = bhs % hsplit;
+  const int bh = bhs / hsplit;
+  const int b = bh / (int)a.heads_kv, hk = bh % (int)a.heads_kv;
+  const unsigned gw = grp.n ? grp_sel(grp, gi) : 0u;
+  const int nblk_wg = grp.n ? (int)((grp.cnt >> (4 * gi)) & 15ull) : 1;
+  const unsigned delta_off = (unsigned)((const char*)delta_g - (const char*)sinit_g);  // same workspace
+  const unsigned ring_lds = (unsigned)__builtin_amdgcn_readfirstlane((int)lds_addr(smem));
+#pragma clang loop unroll(disable)
+  for (int jb = 0; jb < nblk_wg; ++jb) {
+#if PICO_KVP_STAMP
+    tblk = __builtin_amdgcn_s_memtime();
+#endif
+    const int kb = grp.n ? (int)((gw >> (8 * jb)) & 255u) : gi;
+    if (jb > 0) lds_barrier();
+    int lane_l = lane0;
+    asm volatile("" : "+v"(lane_l));
+    const int lane = lane_l, r = lane & 31, h = lane >> 5;
+    const int k0 = kb * KB;
+    const int kw = k0 + 32 * wave;
+    const int qstart = CAUSAL ? k0 : 0;  // k0 is a multiple of QT2
+    const int nqt = Sq > qstart ? (Sq - qstart + QT2 - 1) / QT2 : 0;
+    const int ntot = G * nqt;
+    const int tb = (int)((int64_t)ntot * hs / hsplit);
+    const int ntiles = (int)((int64_t)ntot * (hs + 1) / hsplit) - tb;
+    const int hq0 = hk * G + (nqt ? tb / nqt : 0), q00 = qstart + (nqt ? tb % nqt : 0) * QT2;
+
+    // ---- tile DMA: this wave's image pieces i = 0..PPW-1 (Q: i < PPW/2, dO after) are image pieces
+    // (wave + 4 i) % NQP; wave 0 also issues the LSE / delta piece ----
+    const int64_t qs1 = a.q_strides[1] * 2, ds1 = a.do_strides[1] * 2;  // bytes per query row
+    const char* const qbase = (const char*)((const bf16_t*)a.q + b * a.q_strides[0]);
+    const char* const dobase = (const char*)((const bf16_t*)a.dout + b * a.do_strides[0]);
+    // piece jj of an image = LDS bytes [1024 jj, 1024 jj + 1024): lane l lands 16 bytes at 1024 jj + 16 l, i.e. row
+    // 8 (jj >> 1) + ((l & 31) >> 2), chunk 4 (2 (jj & 1) + (l >> 5)) + ((l & 3) ^ ((row >> 2) & 3)) of kv2_off
+    auto piece_row = [&](int jj, int l) __attribute__((always_inline)) { return 8 * (jj >> 1) + ((l & 31) >> 2); };
+    auto piece_ch = [&](int jj, int l, int row) __attribute__((always_inline)) {
+      return 4 * (2 * (jj & 1) + (l >> 5)) + ((l & 3) ^ ((row >> 2) & 3));
+    };
+    unsigned pc_off[PPW];
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const int jj = (wave + 4 * i) % C::NQP;
+      const int row = piece_row(jj, lane);
+      pc_off[i] = (unsigned)(row * (i < PPW / 2 ? qs1 : ds1) + 16 * piece_ch(jj, lane, row));
+    }
+    struct Tc {
+      int hq, q0;
+      const char* qp;
+      const char* dp;
+      const char* lp;
+    };
+    auto make_tc = [&](int hq, int q0) __attribute__((always_inline)) {
+      Tc c;
+      c.hq = hq;
+      c.q0 = q0;
+      c.qp = qbase + hq * a.q_strides[2] * 2 + q0 * qs1;
+      c.dp = dobase + hq * a.do_strides[2] * 2 + q0 * ds1;
+      c.lp = (const char*)(sinit_g + ((int64_t)b * Hq + hq) * sq_pad + q0);
+      return c;
+    };
+    const int qend = qstart + nqt * QT2;
+    auto advance = [&](Tc& c) __attribute__((always_inline)) {
+      if (c.q0 + QT2 >= qend) {
+        c = make_tc(c.hq + 1, qstart);
+      } else {
+        c.q0 += QT2;
+        c.qp += QT2 * qs1;
+        c.dp += QT2 * ds1;
+        c.lp += QT2 * 4;
+      }
+    };
+    const bool ragged = Sq % QT2 != 0;
+    auto issue_piece = [&](int si, const Tc& c, int i) __attribute__((always_inline)) {
+      const unsigned dst = ring_lds + (unsigned)si * (unsigned)C::SLOT;
+      if (i < PPW) {
+        const int jj = (wave + 4 * i) % C::NQP;
+        unsigned off = pc_off[i];
+        if (ragged && c.q0 + QT2 > Sq) {  // partial tile: rows past Sq - 1 clamped (finite; their LSE is +inf)
+          int l2 = lane0;
+          asm volatile("" : "+v"(l2));
+          const int row = piece_row(jj, l2 & 63);
+          off = (unsigned)((min(c.q0 + row, Sq - 1) - c.q0) * (i < PPW / 2 ? qs1 : ds1) +
+                           16 * piece_ch(jj, l2 & 63, row));
+        }
+        dma_piece(i < PPW / 2 ? c.qp : c.dp, off, dst + (i < PPW / 2 ? 0u : (unsigned)C::QIMG) + (unsigned)jj * 1024u);
+      } else if (wave == 0) {
+        int l = lane0;
+        asm volatile("" : "+v"(l));
+        l &= 31;
+        dma_piece(c.lp, (unsigned)(16 * (l & 15)) + ((l >> 4) ? delta_off : 0u), dst + 2u * C::QIMG);
+      }
+    };
+    Tc nxt = make_tc(hq0, q00);
+#pragma unroll
+    for (int j = 0; j < C::PD; ++j) {
+      if (j < ntiles) {
+#pragma unroll
+        for (int i = 0; i <= PPW; ++i) issue_piece(j, nxt, i);
+      }
+      advance(nxt);
+    }
+
+    // ---- K, V fragments of this wave's 32 keys (B operands of S and dP) ----
+    const bf16_t* kg = (const bf16_t*)a.k + b * a.k_strides[0] + hk * a.k_strides[2];
+    const bf16_t* vg = (const bf16_t*)a.v + b * a.v_strides[0] + hk * a.v_strides[2];
+    bf16x8 kf[KS], vf[KS];
+    {
+      const int key = kw + r;
+      const bool ok = key < Sk;
+      const bf16_t* kp = kg + (int64_t)min(key, Sk - 1) * a.k_strides[1] + 8 * h;
+      const bf16_t* vp = vg + (int64_t)min(key, Sk - 1) * a.v_strides[1] + 8 * h;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const u16x8 kv = *reinterpret_cast<const u16x8*>(kp + 16 * ks);
+        const u16x8 vv = *reinterpret_cast<const u16x8*>(vp + 16 * ks);
+        kf[ks] = __builtin_bit_cast(bf16x8, ok ? kv : (u16x8)0);
+        vf[ks] = __builtin_bit_cast(bf16x8, ok ? vv : (u16x8)0);
+      }
+    }
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) asm volatile("" : "+v"(kf[ks]), "+v"(vf[ks]));
+    f32x16 dk[DT], dv[DT];
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      dk[dt] = (f32x16)0.f;
+      dv[dt] = (f32x16)0.f;
+    }
+    // row-read bases by k-step parity (k-step ks adds 512 (ks >> 1), half X 8192), transposed-read bases of rows
+    // 4 hh + q and + 8 (tile dt adds 512 dt, 16-row step st 4096 st, half X 8192)
+    unsigned qo[2], tro[2];
+    {
+      const int g = lane >> 4, i = lane & 15, hh = g >> 1, q = i >> 2, p = i & 3;
+      qo[0] = kv2_off(r, h);
+      qo[1] = kv2_off(r, 2 + h);
+      tro[0] = kv2_off(4 * hh + q, 2 * (g & 1) + (p >> 1)) + 8 * (p & 1);
+      tro[1] = kv2_off(4 * hh + q + 8, 2 * (g & 1) + (p >> 1)) + 8 * (p & 1);
+    }
+    const bool kpad = kw + 31 >= Sk;  // wave-uniform: some of the wave's keys are padding
+    const int mykey = kw + r;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+#if PICO_KVP_STAMP
+    ph[8] += __builtin_amdgcn_s_memtime() - tblk;
+#endif
+
+    auto init_rows = [&](const float* lsd, int X, int which) __attribute__((always_inline)) {
+      f32x16 v;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 t4 = *reinterpret_cast<const f32x4*>(lsd + 64 * which + 32 * X + 8 * g + 4 * h);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[4 * g + j] = t4[j];
+      }
+      return v;
+    };
+    auto mask_rows = [&](f32x16& sv, int qrow0) __attribute__((always_inline)) {
+      const int rel = mykey >= Sk ? 1 << 30 : (CAUSAL ? mykey - qrow0 - 4 * h : -1);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sv[i] = ((i & 3) + 8 * (i >> 2) < rel) ? -INFINITY : sv[i];
+    };
+    auto vpair = [&](const f32x16& sv, const f32x16& dpv, int e, unsigned& pw, unsigned& sw) __attribute__((always_inline)) {
+      typedef __attribute__((ext_vector_type(2))) float f32x2;
+      typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+      const float p0 = fast_exp2(sv[2 * e] * c2), p1 = fast_exp2(sv[2 * e + 1] * c2);
+      pw = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){p0, p1}, bf16x2));
+      sw = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){p0 * dpv[2 * e], p1 * dpv[2 * e + 1]}, bf16x2));
+    };
+    auto pk4 = [&](const unsigned* w) __attribute__((always_inline)) {
+      typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+      return __builtin_bit_cast(bf16x8, (u32x4){w[0], w[1], w[2], w[3]});
+    };
+
+    int q0cur = q00;
+    for (int t0 = 0; t0 < ntiles; t0 += C::NBUF) {  // unrolled by the ring depth: slot offsets are immediates
+#pragma unroll
+    for (int u = 0; u < C::NBUF; ++u) {
+      const int t = t0 + u;
+      if (t >= ntiles) break;
+#if PICO_KVP_STAMP
+      tlast = __builtin_amdgcn_s_memtime();
+      ph[7] += 1;
+#endif
+      if (t > 0) {
+        if (t + 1 < ntiles) {  // this wave's pieces of tile t landed; tile t + 1's stay in flight
+          if (wave == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW + 1) : "memory");
+          else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");
+        } else {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        KV2_ST(0);
+        lds_barrier();  // every wave's pieces of tile t visible; the slot of tile t - 1 is no longer read
+        KV2_ST(1);
+      }
+      const bool dma_next = t + C::PD < ntiles;
+      const int dslot = (u + C::PD) % C::NBUF;  // a constant after unrolling
+      const char* qs = smem + u * C::SLOT;
+      const char* dos = qs + C::QIMG;
+      const float* lsd = (const float*)(qs + 2 * C::QIMG);
+      const bool diag = (CAUSAL && kw + 31 > q0cur) || kpad;        // half A has masked elements
+      const bool diagB = (CAUSAL && kw + 31 > q0cur + 32) || kpad;  // half B has masked elements
+      KV2_SLOT();
+
+      // M1 operands of half X, read in slot order: [Q k-steps 0..KS-1, dO k-steps 0..KS-1]
+      bf16x8 opA[2 * KS], opB[2 * KS];
+      auto rd_op = [&](bf16x8 (&op)[2 * KS], int X, int k) __attribute__((always_inline)) {
+        op[k] = lds_read_b128((k < KS ? qs : dos) + 512 * ((k % KS) >> 1) + 8192 * X, qo[k & 1]);
+      };
+      // M2 operands of half X: [st][dt] -> (dO^T, Q^T) pairs, read in slot order k = 2 (DT st + dt) + {0: dO^T, 1: Q^T}
+      bf16x8 toA[2][DT], tqA[2][DT], toB[2][DT], tqB[2][DT];
+      auto rd_tr = [&](bf16x8 (&to)[2][DT], bf16x8 (&tq)[2][DT], int X, int k) __attribute__((always_inline)) {
+        const int st = k / (2 * DT), dt = (k / 2) % DT;
+        const char* base = ((k & 1) ? qs : dos) + 8192 * X + 4096 * st + 512 * dt;
+        if (k & 1) tq[st][dt] = tr_pair(base, tro[0], tro[1]);
+        else to[st][dt] = tr_pair(base, tro[0], tro[1]);
+      };
+      unsigned pwA[8], swA[8], pwB[8], swB[8];
+
+      // ---- M1(A): S_A (k < KS), dP_A (k >= KS); operands two slots ahead; B's first operands + initial values ----
+      f32x16 sA = init_rows(lsd, 0, 0), dpA = init_rows(lsd, 0, 1);
+      if (diag) mask_rows(sA, q0cur);
+      rd_op(opA, 0, 0);
+      rd_op(opA, 0, 1);
+      f32x16 sB, dpB;
+      KV2_SLOT();
+      static_for<2 * KS>([&](auto k_) {
+        constexpr int k = decltype(k_)::value;
+        if constexpr (k < KS) sA = mfma32(opA[k], kf[k], sA);
+        else dpA = mfma32(opA[k], vf[k - KS], dpA);
+        if constexpr (k + 2 < 2 * KS) rd_op(opA, 0, k + 2);
+        else rd_op(opB, 1, k + 2 - 2 * KS);
+        if constexpr (k == 4) sB = init_rows(lsd, 1, 0);
+        if constexpr (k == 6) dpB = init_rows(lsd, 1, 1);
+        if constexpr (k == 8) {
+          if (diagB) mask_rows(sB, q0cur + 32);
+        }
+        KV2_SLOT();
+      });
+      KV2_ST(3);
+      // ---- M1(B): S_B, dP_B | V(A) (one element pair per two slots) + A's transposed operands (one per slot) ----
+      static_for<2 * KS>([&](auto k_) {
+        constexpr int k = decltype(k_)::value;
+        if constexpr (k < KS) sB = mfma32(opB[k], kf[k], sB);
+        else dpB = mfma32(opB[k], vf[k - KS], dpB);
+        if constexpr (k + 2 < 2 * KS) rd_op(opB, 1, k + 2);
+        if constexpr ((k & 1) == 0) vpair(sA, dpA, k / 2, pwA[k / 2], swA[k / 2]);
+        rd_tr(toA, tqA, 0, k);
+        KV2_SLOT();
+      });
+      KV2_ST(4);
+      // ---- M2(A): dV^T += dO^T P, dK^T += Q^T dS over A's rows | V(B) + B's transposed operands ----
+      {
+        const bf16x8 pA[2] = {pk4(pwA), pk4(pwA + 4)}, sAp[2] = {pk4(swA), pk4(swA + 4)};
+        static_for<2 * KS>([&](auto k_) {
+          constexpr int k = decltype(k_)::value;
+          constexpr int st = k / (2 * DT), dt = (k / 2) % DT;
+          if constexpr ((k & 1) == 0) dv[dt] = mfma32(toA[st][dt], pA[st], dv[dt]);
+          else dk[dt] = mfma32(tqA[st][dt], sAp[st], dk[dt]);
+          if constexpr ((k & 1) == 0) vpair(sB, dpB, k / 2, pwB[k / 2], swB[k / 2]);
+          rd_tr(toB, tqB, 1, k);
+          KV2_SLOT();
+        });
+      }
+      KV2_ST(5);
+      // ---- M2(B) | the DMA of tile t + 2 ----
+      {
+        const bf16x8 pB[2] = {pk4(pwB), pk4(pwB + 4)}, sBp[2] = {pk4(swB), pk4(swB + 4)};
+        static_for<2 * KS>([&](auto k_) {
+          constexpr int k = decltype(k_)::value;
+          constexpr int st = k / (2 * DT), dt = (k / 2) % DT;
+          if constexpr ((k & 1) == 0) dv[dt] = mfma32(toB[st][dt], pB[st], dv[dt]);
+          else dk[dt] = mfma32(tqB[st][dt], sBp[st], dk[dt]);
+          if constexpr ((k & 1) == 1) {  // image pieces 0..7 in the odd slots (measured: 2, 4 or all 8 of them
+            if (dma_next) issue_piece(dslot, nxt, k / 2);  // in M2(A)'s slots instead is 0-3 % slower)
+          } else if constexpr (k == 0) {  // the LSE / delta piece
+            if (dma_next) issue_piece(dslot, nxt, PPW);
+          }
+          KV2_SLOT();
+        });
+      }
+      KV2_ST(6);
+      advance(nxt);
+      q0cur = q0cur + QT2 >= qend ? qstart : q0cur + QT2;
+    }
+    }
+#if PICO_KVP_STAMP
+    const unsigned long long tep = __builtin_amdgcn_s_memtime();
+#endif
+
+    // ---- epilogue: lane = key kw + r, register i of tile dt = d 32 dt + acc_row(i, h) ----
+    if (hsplit == 1) {
+      const int key = kw + r;
+      const int kc = min(key, Sk - 1);
+      if (a.flags & PICO_ATTN_ROPE_BWD) {  // rotate back by -theta: pairs (d, d + D/2) = tiles (dt, dt + DT/2)
+        const bf16_t* cp = (const bf16_t*)a.rope_cos + (int64_t)kc * a.rope_stride;
+        const bf16_t* sp = (const bf16_t*)a.rope_sin + (int64_t)kc * a.rope_stride;
+#pragma unroll
+        for (int dt = 0; dt < DT / 2; ++dt)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const u16x4 c4 = *reinterpret_cast<const u16x4*>(cp + 32 * dt + 8 * g + 4 * h);
+            const u16x4 s4 = *reinterpret_cast<const u16x4*>(sp + 32 * dt + 8 * g + 4 * h);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const float cf = bf2f(c4[j]), sn = bf2f(s4[j]);
+              const float x1 = dk[dt][4 * g + j], x2 = dk[dt + DT / 2][4 * g + j];
+              dk[dt][4 * g + j] = x1 * cf + x2 * sn;
+              dk[dt + DT / 2][4 * g + j] = x2 * cf - x1 * sn;
+            }
+          }
+      }
+      bf16_t* dkp = (bf16_t*)a.dk + b * a.dk_strides[0] + hk * a.dk_strides[2] + (int64_t)kc * a.dk_strides[1];
+      bf16_t* dvp = (bf16_t*)a.dv + b * a.dv_strides[0] + hk * a.dv_strides[2] + (int64_t)kc * a.dv_strides[1];
+      store_row_bf16_x16<DT>(dkp, h, key < Sk, [&](int dt, int i) { return dk[dt][i] * scale; });
+      store_row_bf16_x16<DT>(dvp, h, key < Sk, [&](int dt, int i) { return dv[dt][i]; });
+    } else {  // fp32 partials [hs][dK | dV][b][key][hk][D]
+      const int64_t part = a.batch * a.seqlen_k * a.heads_kv * 128;
+      float* pk = dkv_part + (int64_t)(2 * hs) * part + ((int64_t)b * Sk * a.heads_kv + hk) * 128;
+      float* pv = pk + part;
+      const int key = kw + r;
+      if (key < Sk) {
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            f32x4 wk, wv;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              wk[j] = dk[dt][4 * g + j] * scale;
+              wv[j] = dv[dt][4 * g + j];
+            }
+            const int64_t o = (int64_t)key * a.heads_kv * 128 + 32 * dt + 8 * g + 4 * h;
+            *reinterpret_cast<f32x4*>(pk + o) = wk;
+            *reinterpret_cast<f32x4*>(pv + o) = wv;
+          }
+      }
+    }
+#if PICO_KVP_STAMP
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    ph[9] += __builtin_amdgcn_s_memtime() - tep;
+#endif
+  }  // key blocks of the group
+#if PICO_KVP_STAMP
+  ph[11] = __builtin_amdgcn_s_memrealtime();
+  ph[13] = __builtin_amdgcn_s_memtime();
+  if ((threadIdx.x & 63) == 0 && (int64_t)blockIdx.x * 4 + wave < STAMP_BYTES / 128) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) stamp_out[((int64_t)blockIdx.x * 4 + wave) * 16 + i] = ph[i];
+  }
+#else
+  (void)stamp_out;
+#endif
+}
+#undef KV2_SLOT
+#undef KV2_ST
+
+// attn_bwd_kvp128_kernel for head_dim 128 (pico_select(PICO_SEL_ATTN_KVP, 0 / 1) forces the 32-row kernel or it)
+bool kvp128_enabled(const pico_attn_args* a) {
+  if (a->head_dim != 128) return false;
+  const int e = pico_sel(PICO_SEL_ATTN_KVP);
+  if (e != PICO_SEL_AUTO) return e != 0;
+  return true;
+}
+#endif  // PICO_SPLIT_D128_TU
+
 // keys per dK/dV workgroup block
 int kv_block(const pico_attn_args* a) {
 #ifndef PICO_SPLIT_D128_TU
@@ -1502,7 +1931,7 @@ int launch_split(const pico_attn_args* a, hipStream_t s) {
 #ifndef PICO_SPLIT_D128_TU
   const bool use_kvp = D == 64 && kvp_enabled(a);
 #else
-  constexpr bool use_kvp = false;
+  const bool use_kvp = D == 128 && kvp128_enabled(a);  // attn_bwd_kvp128_kernel: the -LSE/scale workspace form
 #endif
   const int nmb = (int)((a->seqlen_q + QB - 1) / QB);
   const int64_t gq = (int64_t)nmb * a->batch * a->heads_q;
@@ -1524,6 +1953,12 @@ int launch_split(const pico_attn_args* a, hipStream_t s) {
                          stamps));
   } else if (use_kvp) {
     PICO_TRY(pico_launch(PICO_K_ATTN_BWD_KV, "attn_bwd_kv", attn_bwd_kvp_kernel<CAUSAL, 2, 4>, dim3((int)nblk),
+                         dim3(4 * 64), 0, s, *a, a->softmax_scale, sl2, lse2, delta, sq_pad, hsplit, dkv_part, kg,
+                         stamps));
+  } else
+#else
+  if (use_kvp) {
+    PICO_TRY(pico_launch(PICO_K_ATTN_BWD_KV, "attn_bwd_kv", attn_bwd_kvp128_kernel<CAUSAL>, dim3((int)nblk),
                          dim3(4 * 64), 0, s, *a, a->softmax_scale, sl2, lse2, delta, sq_pad, hsplit, dkv_part, kg,
                          stamps));
   } else

@@ -429,10 +429,28 @@ def test_attention_bwd_d64_kv_kernels(monkeypatch, B, Sq, Sk, Hq, Hkv, causal, m
     """D = 64 dK/dV: attn_bwd_kvp_kernel (64-row query tiles, 4 or 8 waves x 32 keys per workgroup: the default up
     to 4096 keys) and the 32-row attn_bwd_kv_kernel (pico_select PICO_SEL_ATTN_KVP / PICO_SEL_KVP_WAVES force each), each
     with its matching dQ-kernel LSE form, vs an fp32 torch reference, and within bf16 rounding of each other."""
+    _check_kv_kernels(64, ("0", "1", "1w8"), B, Sq, Sk, Hq, Hkv, causal, mode)
+
+
+@pytest.mark.parametrize("B,Sq,Sk,Hq,Hkv,causal,mode", [
+    (4, 1024, 1024, 16, 16, True, "bf16"),   # C4 per tp-2 rank (Llama-2-7B), micro-batch 4
+    (1, 1000, 1000, 8, 2, True, "bf16"),     # ragged, GQA 4, key blocks split over workgroups (hsplit)
+    (2, 1024, 1024, 32, 8, True, "rope"),    # GQA 4, fused RoPE^-1
+    (1, 520, 520, 4, 4, True, "f32acc"),     # caller's fp32 dQ
+    (2, 96, 200, 4, 4, False, "bf16"),       # cross lengths, non-causal
+    (1, 640, 640, 4, 4, False, "rope"),
+])
+def test_attention_bwd_d128_kv_kernels(B, Sq, Sk, Hq, Hkv, causal, mode):
+    """D = 128 dK/dV: attn_bwd_kvp128_kernel (64-row query tiles in halves, one wave per SIMD: the default) and the
+    32-row attn_bwd_kv_kernel<128> (pico_select PICO_SEL_ATTN_KVP 0), each with its dQ-kernel LSE form, vs an fp32
+    torch reference and within bf16 rounding of each other."""
+    _check_kv_kernels(128, ("0", "1"), B, Sq, Sk, Hq, Hkv, causal, mode)
+
+
+def _check_kv_kernels(D, variants, B, Sq, Sk, Hq, Hkv, causal, mode):
     from picotron_amd.model import get_cos_sin
     ops = _ops()
-    torch.manual_seed(Sq * 3 + Sk + Hq + Hkv)
-    D = 64
+    torch.manual_seed(Sq * 3 + Sk + Hq + Hkv + D)
     q, do = [torch.randn(B, Sq, Hq, D, dtype=BF, device=DEV) for _ in range(2)]
     k, v = [torch.randn(B, Sk, Hkv, D, dtype=BF, device=DEV) for _ in range(2)]
     sc = 1.0 / math.sqrt(D)
@@ -456,7 +474,7 @@ def test_attention_bwd_d64_kv_kernels(monkeypatch, B, Sq, Sk, Hq, Hkv, causal, m
         gq, gk = rq.float(), rk.float()
     res = {}
     from picotron_amd import _lib as L
-    for kvp in ("0", "1", "1w8"):
+    for kvp in variants:
         L.select(L.SEL_ATTN_KVP, int(kvp[0]))
         L.select(L.SEL_KVP_WAVES, 8 if kvp.endswith("w8") else 4)
         if mode == "bf16":
@@ -474,7 +492,7 @@ def test_attention_bwd_d64_kv_kernels(monkeypatch, B, Sq, Sk, Hq, Hkv, causal, m
         res[kvp] = [t.float() for t in (dq, dk, dv)]
         for a, b in zip(res[kvp], (gq, gk, gv)):
             assert rel_l2(a, b) < 1e-2, (kvp, rel_l2(a, b))
-    for other in ("1", "1w8"):
+    for other in variants[1:]:
         for a, b in zip(res["0"], res[other]):
             assert rel_l2(a, b) < 8e-3
 
