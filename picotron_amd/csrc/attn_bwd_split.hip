@@ -1359,7 +1359,7 @@ __global__ __launch_bounds__(NW * 64, MINB) void attn_bwd_kvp_kernel(const pico_
 bool kvp_enabled(const pico_attn_args* a) {
   if (a->head_dim != 64) return false;
   const int e = pico_sel(PICO_SEL_ATTN_KVP);
-  if (e != PICO_SEL_AUTO) return e == 1;
+  if (e != PICO_SEL_AUTO) return e != 0;
   return a->seqlen_k <= (a->causal ? 1536 : 4096);
 }
 
@@ -1373,419 +1373,6 @@ int kvp_waves(const pico_attn_args* a) {
   return !a->causal && a->seqlen_k >= 2048 ? 8 : 4;
 }
 
-// ------------------------------------------------------------------------------------------------
-// dK / dV kernel, D = 64, 64 keys per wave, one wave per SIMD (round 6)
-// ------------------------------------------------------------------------------------------------
-// attn_bwd_kvp128_kernel's one-wave-per-SIMD form at head_dim 64: a wave owns 64 keys as two 32-key halves c (dK /
-// dV of both in 128 accumulator registers, K / V fragments resident), a workgroup 4 waves = a 256-key block, one
-// workgroup per CU. Each 64-row ring tile splits into row halves X = A / B, so a tile is four units (X, c) of
-// 8 M1 MFMAs (S^T, dP^T of 32 keys x 32 rows) and 8 M2 MFMAs (dV^T, dK^T of 32 keys), 64 MFMAs per wave and tile, in
-// eight 8-slot segments M1(A0) M1(A1) M1(B0) M1(B1) M2(A0) M2(A1) M2(B0) M2(B1). Against attn_bwd_kvp_kernel
-// (32 keys per wave, two waves per SIMD) every Q / dO fragment, transposed operand and LDS-DMA byte serves twice
-// the keys. The softmax VALU (32 element pairs per tile) streams through slots 10..55 in unit order, each unit's
-// pairs after its M1 and before its M2; the LDS images use the 8-row x 32-column subtile layout (kvw_off).
-struct KVWCfg {
-  static constexpr int D = 64, KS = 4, DT = 2;
-  static constexpr int QIMG = QT2 * 128;         // one Q (or dO) 64-row image, 8 KiB
-  static constexpr int LSD = 1024;               // -LSE/scale [64] | -delta [64] (+ 512 B the DMA piece repeats)
-  static constexpr int SLOT = 2 * QIMG + LSD;    // 17 KiB
-  static constexpr int NBUF = 3, PD = NBUF - 1;  // 51 KiB per workgroup, prefetch distance 2
-  static constexpr int NQP = QIMG / 1024;        // 8 pieces per image
-  static constexpr int PPW = 2 * NQP / 4;        // 4 image pieces per wave per tile (+ wave 0's LSE / delta piece)
-};
-
-#define KVW_SLOT() __builtin_amdgcn_sched_barrier(0)
-
-// byte offset of 16-byte chunk ch (0..7) of row `row` in a [64][64 x bf16] image of 8-row x 32-column subtiles of
-// 512 B (cdna_hip_programming.md T11 image (a) at 128-byte rows): the row reads of a k-step parity and the transposed
-// reads of a row parity share one base register each, every other offset an immediate
-PICO_DEV int kvw_off(int row, int ch) {
-  return 1024 * (row >> 3) + 512 * (ch >> 2) + 64 * (row & 7) + 16 * ((ch & 3) ^ ((row >> 2) & 3));
-}
-
-
-template <bool CAUSAL>
-__global__ __launch_bounds__(256, 1) void attn_bwd_kvw_kernel(const pico_attn_args a, float scale, float c2,
-                                                              const float* __restrict__ sinit_g,
-                                                              const float* __restrict__ delta_g, int sq_pad,
-                                                              int hsplit, float* __restrict__ dkv_part,
-                                                              const BlkGroups grp,
-                                                              unsigned long long* __restrict__ stamp_out) {
-  using C = KVWCfg;
-#if PICO_KVP_STAMP  // the stamp words of attn_bwd_kvp_kernel (scripts/kvp_stamps.py): 0 wait, 1 barrier, 3-6 phases
-  unsigned long long ph[16] = {0}, tlast = 0, tblk = 0;
-  ph[10] = __builtin_amdgcn_s_memrealtime();
-  ph[12] = __builtin_amdgcn_s_memtime();
-#define KVW_ST(i)                                               \
-  {                                                             \
-    const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
-    ph[i] += t_ - tlast;                                        \
-    tlast = t_;                                                 \
-  }
-#else
-#define KVW_ST(i)
-#endif
-  constexpr int KS = C::KS, DT = C::DT, PPW = C::PPW, NW = 4, KB = 64 * NW;
-  static_assert(PPW == 4 && 2 * C::NQP == PPW * NW, "4 image pieces per wave");
-  __shared__ __attribute__((aligned(16))) char smem[C::NBUF * C::SLOT];
-
-  const int lane0 = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int Sq = (int)a.seqlen_q, Sk = (int)a.seqlen_k;
-  const int Hq = (int)a.heads_q;
-  const int G = (int)(a.heads_q / a.heads_kv);
-  const int nbh = (int)(a.batch * a.heads_kv) * hsplit;
-  const int gi = blockIdx.x / nbh;
-  const int bhs = blockIdx.x % nbh;
-  const int hs = bhs % hsplit;
-  const int bh = bhs / hsplit;
-  const int b = bh / (int)a.heads_kv, hk = bh % (int)a.heads_kv;
-  const unsigned gw = grp.n ? grp_sel(grp, gi) : 0u;
-  const int nblk_wg = grp.n ? (int)((grp.cnt >> (4 * gi)) & 15ull) : 1;
-  const unsigned delta_off = (unsigned)((const char*)delta_g - (const char*)sinit_g);  // same workspace
-  const unsigned ring_lds = (unsigned)__builtin_amdgcn_readfirstlane((int)lds_addr(smem));
-#pragma clang loop unroll(disable)
-  for (int jb = 0; jb < nblk_wg; ++jb) {
-#if PICO_KVP_STAMP
-    tblk = __builtin_amdgcn_s_memtime();
-#endif
-    const int kb = grp.n ? (int)((gw >> (8 * jb)) & 255u) : gi;
-    if (jb > 0) lds_barrier();
-    int lane_l = lane0;
-    asm volatile("" : "+v"(lane_l));
-    const int lane = lane_l, r = lane & 31, h = lane >> 5;
-    const int k0 = kb * KB;
-    const int kw = k0 + 64 * wave;
-    const int qstart = CAUSAL ? k0 : 0;  // k0 is a multiple of QT2
-    const int nqt = Sq > qstart ? (Sq - qstart + QT2 - 1) / QT2 : 0;
-    const int ntot = G * nqt;
-    const int tb = (int)((int64_t)ntot * hs / hsplit);
-    const int ntiles = (int)((int64_t)ntot * (hs + 1) / hsplit) - tb;
-    const int hq0 = hk * G + (nqt ? tb / nqt : 0), q00 = qstart + (nqt ? tb % nqt : 0) * QT2;
-
-    // ---- tile DMA: this wave's pieces i = 0..3 are Q pieces wave, wave + 4 and dO pieces wave, wave + 4 (piece jj =
-    // image rows 8 jj .. 8 jj + 7: lane l lands 16 bytes at 1024 jj + 16 l = row 8 jj + ((l & 31) >> 2), chunk
-    // 4 (l >> 5) + ((l & 3) ^ ((row >> 2) & 3)) of kvw_off); wave 0 also issues the LSE / delta piece ----
-    const int64_t qs1 = a.q_strides[1] * 2, ds1 = a.do_strides[1] * 2;  // bytes per query row
-    const char* const qbase = (const char*)((const bf16_t*)a.q + b * a.q_strides[0]);
-    const char* const dobase = (const char*)((const bf16_t*)a.dout + b * a.do_strides[0]);
-    auto piece_row = [&](int jj, int l) __attribute__((always_inline)) { return 8 * jj + ((l & 31) >> 2); };
-    auto piece_ch = [&](int l, int row) __attribute__((always_inline)) {
-      return 4 * (l >> 5) + ((l & 3) ^ ((row >> 2) & 3));
-    };
-    unsigned pc_off[PPW];
-#pragma unroll
-    for (int i = 0; i < PPW; ++i) {
-      const int jj = wave + 4 * (i & 1);
-      const int row = piece_row(jj, lane);
-      pc_off[i] = (unsigned)(row * (i < 2 ? qs1 : ds1) + 16 * piece_ch(lane, row));
-    }
-    struct Tc {
-      int hq, q0;
-      const char* qp;
-      const char* dp;
-      const char* lp;
-    };
-    auto make_tc = [&](int hq, int q0) __attribute__((always_inline)) {
-      Tc c;
-      c.hq = hq;
-      c.q0 = q0;
-      c.qp = qbase + hq * a.q_strides[2] * 2 + q0 * qs1;
-      c.dp = dobase + hq * a.do_strides[2] * 2 + q0 * ds1;
-      c.lp = (const char*)(sinit_g + ((int64_t)b * Hq + hq) * sq_pad + q0);
-      return c;
-    };
-    const int qend = qstart + nqt * QT2;
-    auto advance = [&](Tc& c) __attribute__((always_inline)) {
-      if (c.q0 + QT2 >= qend) {
-        c = make_tc(c.hq + 1, qstart);
-      } else {
-        c.q0 += QT2;
-        c.qp += QT2 * qs1;
-        c.dp += QT2 * ds1;
-        c.lp += QT2 * 4;
-      }
-    };
-    const bool ragged = Sq % QT2 != 0;
-    auto issue_piece = [&](int si, const Tc& c, int i) __attribute__((always_inline)) {
-      const unsigned dst = ring_lds + (unsigned)si * (unsigned)C::SLOT;
-      if (i < PPW) {
-        const int jj = wave + 4 * (i & 1);
-        unsigned off = pc_off[i];
-        if (ragged && c.q0 + QT2 > Sq) {  // partial tile: rows past Sq - 1 clamped (finite; their LSE is +inf)
-          int l2 = lane0;
-          asm volatile("" : "+v"(l2));
-          const int row = piece_row(jj, l2 & 63);
-          off = (unsigned)((min(c.q0 + row, Sq - 1) - c.q0) * (i < 2 ? qs1 : ds1) + 16 * piece_ch(l2 & 63, row));
-        }
-        dma_piece(i < 2 ? c.qp : c.dp, off, dst + (i < 2 ? 0u : (unsigned)C::QIMG) + (unsigned)jj * 1024u);
-      } else if (wave == 0) {
-        int l = lane0;
-        asm volatile("" : "+v"(l));
-        l &= 31;
-        dma_piece(c.lp, (unsigned)(16 * (l & 15)) + ((l >> 4) ? delta_off : 0u), dst + 2u * C::QIMG);
-      }
-    };
-    Tc nxt = make_tc(hq0, q00);
-#pragma unroll
-    for (int j = 0; j < C::PD; ++j) {
-      if (j < ntiles) {
-#pragma unroll
-        for (int i = 0; i <= PPW; ++i) issue_piece(j, nxt, i);
-      }
-      advance(nxt);
-    }
-
-    // ---- K, V fragments of this wave's two 32-key halves (B operands of S and dP) ----
-    const bf16_t* kg = (const bf16_t*)a.k + b * a.k_strides[0] + hk * a.k_strides[2];
-    const bf16_t* vg = (const bf16_t*)a.v + b * a.v_strides[0] + hk * a.v_strides[2];
-    bf16x8 kf[2][KS], vf[2][KS];
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const int key = kw + 32 * c + r;
-      const bool ok = key < Sk;
-      const bf16_t* kp = kg + (int64_t)min(key, Sk - 1) * a.k_strides[1] + 8 * h;
-      const bf16_t* vp = vg + (int64_t)min(key, Sk - 1) * a.v_strides[1] + 8 * h;
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        const u16x8 kv = *reinterpret_cast<const u16x8*>(kp + 16 * ks);
-        const u16x8 vv = *reinterpret_cast<const u16x8*>(vp + 16 * ks);
-        kf[c][ks] = __builtin_bit_cast(bf16x8, ok ? kv : (u16x8)0);
-        vf[c][ks] = __builtin_bit_cast(bf16x8, ok ? vv : (u16x8)0);
-        asm volatile("" : "+a"(kf[c][ks]), "+a"(vf[c][ks]));  // resident in AGPRs, MFMA B operands from there
-      }
-    }
-    f32x16 dk[2][DT], dv[2][DT];
-#pragma unroll
-    for (int c = 0; c < 2; ++c)
-#pragma unroll
-      for (int dt = 0; dt < DT; ++dt) {
-        dk[c][dt] = (f32x16)0.f;
-        dv[c][dt] = (f32x16)0.f;
-      }
-    // row-read bases by k-step parity (k-step ks adds 512 (ks >> 1), half X 4096), transposed-read bases of rows
-    // 4 hh + q and + 8 (tile dt adds 512 dt, 16-row step st 2048 st, half X 4096)
-    unsigned qo[2], tro[2];
-    {
-      const int g = lane >> 4, i = lane & 15, hh = g >> 1, q = i >> 2, p = i & 3;
-      qo[0] = kvw_off(r, h);
-      qo[1] = kvw_off(r, 2 + h);
-      tro[0] = kvw_off(4 * hh + q, 2 * (g & 1) + (p >> 1)) + 8 * (p & 1);
-      tro[1] = kvw_off(4 * hh + q + 8, 2 * (g & 1) + (p >> 1)) + 8 * (p & 1);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-#if PICO_KVP_STAMP
-    ph[8] += __builtin_amdgcn_s_memtime() - tblk;
-#endif
-
-    auto init_rows = [&](const float* lsd, int X, int which) __attribute__((always_inline)) {
-      f32x16 v;
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const f32x4 t4 = *reinterpret_cast<const f32x4*>(lsd + 64 * which + 32 * X + 8 * g + 4 * h);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[4 * g + j] = t4[j];
-      }
-      return v;
-    };
-    // diagonal / padding-key mask on an S initial value of key half c: -inf where key > query row or key >= Sk
-    auto mask_rows = [&](f32x16& sv, int qrow0, int c) __attribute__((always_inline)) {
-      const int mykey = kw + 32 * c + r;
-      const int rel = mykey >= Sk ? 1 << 30 : (CAUSAL ? mykey - qrow0 - 4 * h : -1);
-#pragma unroll
-      for (int i = 0; i < 16; ++i) sv[i] = ((i & 3) + 8 * (i >> 2) < rel) ? -INFINITY : sv[i];
-    };
-    auto vpair = [&](const f32x16& sv, const f32x16& dpv, int e, unsigned& pw, unsigned& sw) __attribute__((always_inline)) {
-      typedef __attribute__((ext_vector_type(2))) float f32x2;
-      typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
-      const float p0 = fast_exp2(sv[2 * e] * c2), p1 = fast_exp2(sv[2 * e + 1] * c2);
-      pw = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){p0, p1}, bf16x2));
-      sw = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){p0 * dpv[2 * e], p1 * dpv[2 * e + 1]}, bf16x2));
-    };
-    auto pk4 = [&](const unsigned* w) __attribute__((always_inline)) {
-      typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
-      return __builtin_bit_cast(bf16x8, (u32x4){w[0], w[1], w[2], w[3]});
-    };
-
-    int q0cur = q00;
-    for (int t0 = 0; t0 < ntiles; t0 += C::NBUF) {  // unrolled by the ring depth: slot offsets are immediates
-#pragma unroll
-    for (int u = 0; u < C::NBUF; ++u) {
-      const int t = t0 + u;
-      if (t >= ntiles) break;
-#if PICO_KVP_STAMP
-      tlast = __builtin_amdgcn_s_memtime();
-      ph[7] += 1;
-#endif
-      if (t > 0) {
-        if (t + 1 < ntiles) {  // this wave's pieces of tile t landed; tile t + 1's stay in flight
-          if (wave == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW + 1) : "memory");
-          else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");
-        } else {
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        KVW_ST(0);
-        lds_barrier();  // every wave's pieces of tile t visible; the slot of tile t - 1 is no longer read
-        KVW_ST(1);
-      }
-      const bool dma_next = t + C::PD < ntiles;
-      const int dslot = (u + C::PD) % C::NBUF;  // a constant after unrolling
-      const char* qs = smem + u * C::SLOT;
-      const char* dos = qs + C::QIMG;
-      const float* lsd = (const float*)(qs + 2 * C::QIMG);
-      // unit (X, c) has masked elements: some key of half c above some row of half X, or padding keys
-      bool dg[2][2];
-#pragma unroll
-      for (int X = 0; X < 2; ++X)
-#pragma unroll
-        for (int c = 0; c < 2; ++c) dg[X][c] = (CAUSAL && kw + 32 * c + 31 > q0cur + 32 * X) || kw + 32 * c + 31 >= Sk;
-      KVW_SLOT();
-
-      // M1 operands of half X, [Q k-steps 0..3, dO k-steps 0..3]; M2 operands [st][dt] (dO^T, Q^T)
-      bf16x8 op[2][2 * KS];  // M1 operands of half X: [Q k-steps 0..3, dO k-steps 0..3]
-      auto rd_op = [&](int X, int k) __attribute__((always_inline)) {
-        op[X][k] = lds_read_b128((k < KS ? qs : dos) + 512 * ((k % KS) >> 1) + 4096 * X, qo[k & 1]);
-      };
-      bf16x8 to[2][2][DT], tq[2][2][DT];  // M2 operands of half X: [st][dt] (dO^T, Q^T)
-      auto rd_tr = [&](int X, int j) __attribute__((always_inline)) {  // j = 2 (DT st + dt) + {0: dO^T, 1: Q^T}
-        const int st = j / (2 * DT), dt = (j / 2) % DT;
-        const char* base = ((j & 1) ? qs : dos) + 4096 * X + 2048 * st + 512 * dt;
-        if (j & 1) tq[X][st][dt] = tr_pair(base, tro[0], tro[1]);
-        else to[X][st][dt] = tr_pair(base, tro[0], tro[1]);
-      };
-      f32x16 sv[2][2], dpv[2][2];         // unit (X, c) accumulators
-      unsigned pw[2][2][8], sw[2][2][8];  // packed P / dS pairs of unit (X, c)
-      // the tile's 64 slots in four 16-slot phases:
-      //   M1(A) | B's initial values      M1(B) | V(A) + A's transposed reads
-      //   M2(A) | V(B) + B's transposed reads      M2(B) | the DMA of tile t + 2
-      // M1(X) slot j: operand k = j / 2 for both key halves c = j % 2 (each Q / dO fragment read once, 4 slots ahead)
-      auto slot_body = [&](auto s_) __attribute__((always_inline)) {
-        constexpr int s = decltype(s_)::value;
-        constexpr int phase = s / 16, j = s % 16;
-        if constexpr (phase < 2) {
-          constexpr int X = phase, k = j / 2, c = j % 2;
-          if constexpr (k < KS) sv[X][c] = mfma32(op[X][k], kf[c][k], sv[X][c]);
-          else dpv[X][c] = mfma32(op[X][k], vf[c][k - KS], dpv[X][c]);
-        } else {  // M2(X) slot j: key half c = j / 8, then 2 (DT st + dt) + {0: dV, 1: dK}
-          constexpr int X = phase - 2, c = j / 8, jj = j % 8, st = jj / (2 * DT), dt = (jj / 2) % DT;
-          if constexpr ((jj & 1) == 0) dv[c][dt] = mfma32(to[X][st][dt], pk4(&pw[X][c][4 * st]), dv[c][dt]);
-          else dk[c][dt] = mfma32(tq[X][st][dt], pk4(&sw[X][c][4 * st]), dk[c][dt]);
-        }
-        if constexpr ((s & 1) == 0 && s + 4 < 32) rd_op((s + 4) / 16, ((s + 4) % 16) / 2);
-        if constexpr (s == 6) sv[1][0] = init_rows(lsd, 1, 0);
-        if constexpr (s == 7) sv[1][1] = init_rows(lsd, 1, 0);
-        if constexpr (s == 8) dpv[1][0] = dpv[1][1] = init_rows(lsd, 1, 1);
-        if constexpr (s == 9) {
-          if (dg[1][0]) mask_rows(sv[1][0], q0cur + 32, 0);
-          if (dg[1][1]) mask_rows(sv[1][1], q0cur + 32, 1);
-        }
-        if constexpr (phase == 1 && (j & 1) == 1) rd_tr(0, j / 2);
-        if constexpr (phase == 2 && (j & 1) == 1) rd_tr(1, j / 2);
-        if constexpr (phase == 1 || phase == 2) {  // V(X = phase - 1): unit (X, j / 8), element pair j % 8
-          constexpr int X = phase - 1, c = j / 8, e = j % 8;
-          vpair(sv[X][c], dpv[X][c], e, pw[X][c][e], sw[X][c][e]);
-        }
-        if constexpr (s == 48) {
-          if (dma_next) issue_piece(dslot, nxt, PPW);  // the LSE / delta piece
-        }
-        if constexpr (s >= 49 && (s - 49) % 3 == 0 && (s - 49) / 3 < PPW) {
-          if (dma_next) issue_piece(dslot, nxt, (s - 49) / 3);
-        }
-        KVW_SLOT();
-        if constexpr (s == 15) KVW_ST(3);
-        if constexpr (s == 31) KVW_ST(4);
-        if constexpr (s == 47) KVW_ST(5);
-      };
-      // A's initial values and first operands
-      sv[0][0] = init_rows(lsd, 0, 0);
-      sv[0][1] = init_rows(lsd, 0, 0);
-      dpv[0][0] = dpv[0][1] = init_rows(lsd, 0, 1);
-      if (dg[0][0]) mask_rows(sv[0][0], q0cur, 0);
-      if (dg[0][1]) mask_rows(sv[0][1], q0cur, 1);
-      rd_op(0, 0);
-      rd_op(0, 1);
-      KVW_SLOT();
-      static_for<64>(slot_body);
-      KVW_ST(6);
-      advance(nxt);
-      q0cur = q0cur + QT2 >= qend ? qstart : q0cur + QT2;
-    }
-    }
-#if PICO_KVP_STAMP
-    const unsigned long long tep = __builtin_amdgcn_s_memtime();
-#endif
-
-    // ---- epilogue: lane = key kw + 32 c + r, register i of tile dt = d 32 dt + acc_row(i, h) ----
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const int key = kw + 32 * c + r;
-      if (hsplit == 1) {
-        const int kc = min(key, Sk - 1);
-        if (a.flags & PICO_ATTN_ROPE_BWD) {  // rotate back by -theta: pairs (d, d + 32) = tiles (0, 1)
-          const bf16_t* cp = (const bf16_t*)a.rope_cos + (int64_t)kc * a.rope_stride;
-          const bf16_t* sp = (const bf16_t*)a.rope_sin + (int64_t)kc * a.rope_stride;
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const u16x4 c4 = *reinterpret_cast<const u16x4*>(cp + 8 * g + 4 * h);
-            const u16x4 s4 = *reinterpret_cast<const u16x4*>(sp + 8 * g + 4 * h);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              const float cf = bf2f(c4[j]), sn = bf2f(s4[j]);
-              const float x1 = dk[c][0][4 * g + j], x2 = dk[c][1][4 * g + j];
-              dk[c][0][4 * g + j] = x1 * cf + x2 * sn;
-              dk[c][1][4 * g + j] = x2 * cf - x1 * sn;
-            }
-          }
-        }
-        bf16_t* dkp = (bf16_t*)a.dk + b * a.dk_strides[0] + hk * a.dk_strides[2] + (int64_t)kc * a.dk_strides[1];
-        bf16_t* dvp = (bf16_t*)a.dv + b * a.dv_strides[0] + hk * a.dv_strides[2] + (int64_t)kc * a.dv_strides[1];
-        store_row_bf16_x16<DT>(dkp, h, key < Sk, [&](int dt, int i) { return dk[c][dt][i] * scale; });
-        store_row_bf16_x16<DT>(dvp, h, key < Sk, [&](int dt, int i) { return dv[c][dt][i]; });
-      } else if (key < Sk) {  // fp32 partials [hs][dK | dV][b][key][hk][D]
-        const int64_t part = a.batch * a.seqlen_k * a.heads_kv * 64;
-        float* pk = dkv_part + (int64_t)(2 * hs) * part + ((int64_t)b * Sk * a.heads_kv + hk) * 64;
-        float* pv = pk + part;
-#pragma unroll
-        for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            f32x4 wk, wv;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              wk[j] = dk[c][dt][4 * g + j] * scale;
-              wv[j] = dv[c][dt][4 * g + j];
-            }
-            const int64_t o = (int64_t)key * a.heads_kv * 64 + 32 * dt + 8 * g + 4 * h;
-            *reinterpret_cast<f32x4*>(pk + o) = wk;
-            *reinterpret_cast<f32x4*>(pv + o) = wv;
-          }
-      }
-    }
-#if PICO_KVP_STAMP
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    ph[9] += __builtin_amdgcn_s_memtime() - tep;
-#endif
-  }  // key blocks of the group
-#if PICO_KVP_STAMP
-  ph[11] = __builtin_amdgcn_s_memrealtime();
-  ph[13] = __builtin_amdgcn_s_memtime();
-  if ((threadIdx.x & 63) == 0 && (int64_t)blockIdx.x * 4 + wave < STAMP_BYTES / 128) {
-#pragma unroll
-    for (int i = 0; i < 16; ++i) stamp_out[((int64_t)blockIdx.x * 4 + wave) * 16 + i] = ph[i];
-  }
-#else
-  (void)stamp_out;
-#endif
-}
-#undef KVW_SLOT
-#undef KVW_ST
-
-// attn_bwd_kvw_kernel (64 keys per wave) for D = 64: pico_select(PICO_SEL_ATTN_KVP, 2) forces it
-bool kvw_enabled(const pico_attn_args* a) {
-  if (a->head_dim != 64) return false;
-  return pico_sel(PICO_SEL_ATTN_KVP) == 2;
-}
 #endif  // !PICO_SPLIT_D128_TU
 
 #ifdef PICO_SPLIT_D128_TU
@@ -2220,7 +1807,6 @@ bool kvp128_enabled(const pico_attn_args* a) {
 // keys per dK/dV workgroup block
 int kv_block(const pico_attn_args* a) {
 #ifndef PICO_SPLIT_D128_TU
-  if (kvw_enabled(a)) return 256;
   if (kvp_enabled(a)) return 32 * kvp_waves(a);
 #endif
   (void)a;
@@ -2243,7 +1829,6 @@ int64_t split_lsd_floats(const pico_attn_args* a) {
 int kv_minb(const pico_attn_args* a) {
   if (a->head_dim == 128) return 1;
 #ifndef PICO_SPLIT_D128_TU
-  if (kvw_enabled(a)) return 1;                           // attn_bwd_kvw_kernel: one wave per SIMD
   if (kvp_enabled(a)) return kvp_waves(a) == 8 ? 1 : 2;  // attn_bwd_kvp_kernel: two waves per SIMD, <= 256 VGPRs
 #endif
   return a->causal ? 3 : 2;
@@ -2345,8 +1930,7 @@ int launch_split(const pico_attn_args* a, hipStream_t s) {
   float* dkv_part = delta + split_lsd_floats(a);
   const float sl2 = a->softmax_scale * LOG2E;
 #ifndef PICO_SPLIT_D128_TU
-  const bool use_kvw = D == 64 && kvw_enabled(a);
-  const bool use_kvp = use_kvw || (D == 64 && kvp_enabled(a));  // both consume the -LSE/scale workspace form
+  const bool use_kvp = D == 64 && kvp_enabled(a);
 #else
   const bool use_kvp = D == 128 && kvp128_enabled(a);  // attn_bwd_kvp128_kernel: the -LSE/scale workspace form
 #endif
@@ -2364,10 +1948,7 @@ int launch_split(const pico_attn_args* a, hipStream_t s) {
   if (nblk == 0) return 0;
   unsigned long long* stamps = (unsigned long long*)((char*)a->workspace + pico_attn_bwd_split_workspace(a) - STAMP_BYTES);
 #ifndef PICO_SPLIT_D128_TU
-  if (use_kvw) {
-    PICO_TRY(pico_launch(PICO_K_ATTN_BWD_KV, "attn_bwd_kv", attn_bwd_kvw_kernel<CAUSAL>, dim3((int)nblk), dim3(4 * 64),
-                         0, s, *a, a->softmax_scale, sl2, lse2, delta, sq_pad, hsplit, dkv_part, kg, stamps));
-  } else if (use_kvp && kvp_waves(a) == 8) {
+  if (use_kvp && kvp_waves(a) == 8) {
     PICO_TRY(pico_launch(PICO_K_ATTN_BWD_KV, "attn_bwd_kv", attn_bwd_kvp_kernel<CAUSAL, 1, 8>, dim3((int)nblk),
                          dim3(8 * 64), 0, s, *a, a->softmax_scale, sl2, lse2, delta, sq_pad, hsplit, dkv_part, kg,
                          stamps));

@@ -1,6 +1,6 @@
 """dK / dV kernel A/B through pico_select(PICO_SEL_ATTN_KVP, sel): D = 128 sel 0 = the 32-row attn_bwd_kv_kernel<128>,
-1 = attn_bwd_kvp128_kernel; D = 64 sel 0 = 32-row, 1 = attn_bwd_kvp_kernel (32 keys per wave), 2 =
-attn_bwd_kvw_kernel (64 keys per wave). Per config: rel-L2 of dQ / dK / dV against an fp32 torch reference for
+1 = attn_bwd_kvp128_kernel; D = 64 sel 0 = 32-row, 1 = attn_bwd_kvp_kernel (the 64-keys-per-wave kernel that
+took sel 2 was removed after measuring slower, commit 273720e). Per config: rel-L2 of dQ / dK / dV against an fp32 torch reference for
 every selection, each selection's dK / dV against the first's, and the mean launch time of the dK/dV and dQ kernels
 (library HIP-event timer) over --rounds interleaved rounds. One JSON line per config.
 
