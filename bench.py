@@ -254,6 +254,8 @@ def main():
         opt.zero_grad(set_to_none=False)
         train_step(model, loader, device, graphs=None)
         torch.cuda.synchronize()
+        if hasattr(model, "reset"):  # as TrainingStep.reset: the syncing micro-batch left every bucket marked ready
+            model.reset()
     if not args.no_kernel_timing:
         for k in kernel_ids:
             tot, n = L.prof_collect(k)
@@ -264,15 +266,18 @@ def main():
     # Exposed all-reduce time: device events around the syncing micro-batch's bucket all-reduces, over untimed steps
     # AFTER the throughput region (the per-bucket events and waits stay out of the timed steps). Only on
     # RCCL: gloo's Work.wait() blocks the host inside the backward, so its timings would describe the harness.
+    # The steps run on every backend (the gloo tests exercise the same sequence as the RCCL run: kernel-timing step,
+    # then these); only RCCL's timings are reported.
     exposure = None
     if hasattr(model, "comm_timing") and args.comm_steps > 0:
+        model.comm_timing(True)
+        for _ in range(args.comm_steps):
+            step(sync_loss=True)
+        torch.cuda.synchronize()
+        report = model.comm_report()
+        model.comm_timing(False)
         if dist.get_backend() == "nccl":
-            model.comm_timing(True)
-            for _ in range(args.comm_steps):
-                step(sync_loss=True)
-            torch.cuda.synchronize()
-            exposure = comm_exposure(model.comm_report(), world, device)
-            model.comm_timing(False)
+            exposure = comm_exposure(report, world, device)
         else:
             exposure = {"exposed_ms": None, "exposed_over": f"not measured: {dist.get_backend()} backend"}
     allreduce = measure_allreduce(model, world, device) if world > 1 else None
@@ -369,7 +374,8 @@ def main():
                        "schedule": ("eager" if not args.graphs else
                                     "pipelined graph (forward i beside backward i-1)" if pipelined_enabled() else
                                     "graph per micro-batch"),
-                       "wgrad": ("grouped micro-batches (one GEMM per projection per %d micro-batches)" % _WP.group_size()
+                       "wgrad": ("grouped micro-batches (one GEMM per projection per %d micro-batches)" % _WP.group_size(
+                           getattr(model, "module", model).final_proj.weight)
                                  if _WP.enabled() and (not args.graphs or pipelined_enabled()) else "per micro-batch"),
                        "wgrad_group_buffers_gb": round(_WP.footprint_bytes() / 1e9, 2),
                        "peak_memory_gb": round(torch.cuda.max_memory_allocated(device) / 1e9, 1)},

@@ -18,9 +18,9 @@ with no copy: the operands are already adjacent. dW is the same sum, accumulated
 (the pairing is verified per GEMM by pointer, never assumed); a second half whose own operands are elsewhere while
 its first half is pending copies them in and runs the pair GEMM.
 
-PICO_WGRAD_GROUP = G > 2 generalises the pairs to groups of G micro-batches (slot i % G, x^T set (i // G) % 2):
-the first G - 1 defer and the last runs one GEMM over K = G T tokens — and, under DataParallelBucket, one fp32
-read-modify-write of main_grad per G micro-batches instead of per two.
+Groups of G micro-batches (group_size(): 4, or 8 under DataParallelBucket; PICO_WGRAD_GROUP overrides) generalise
+the pairs (slot i % G, x^T set (i // G) % 2): the first G - 1 defer and the last runs one GEMM over K = G T tokens —
+and, under DataParallelBucket, one fp32 read-modify-write of main_grad per G micro-batches instead of per two.
 
 Active only inside train.train_step / PipelinedMicroBatchGraph, which announce each micro-batch
 (`micro_batch(i, n)`), and with PICO_WGRAD_PAIR != 0. Not under MicroBatchGraph: its one captured micro-batch
@@ -51,11 +51,18 @@ def enabled():
     return os.getenv("PICO_WGRAD_PAIR", "1") != "0"
 
 
-def group_size():
-    """PICO_WGRAD_GROUP: micro-batches per weight-gradient GEMM (2 = pairs; 4, the default: one GEMM over four,
-    K = 4T). C2 step, same box, 3 alternating rounds (profiles/r05_ab_wgrad_group.jsonl): 4 vs 2 — 823.7 -> 818.9 ms,
-    under DataParallelBucket 854.3 -> 837.3 ms (half the fp32 main_grad read-modify-writes)."""
-    g = int(os.getenv("PICO_WGRAD_GROUP", "4"))
+def group_size(weight=None):
+    """Micro-batches per weight-gradient GEMM: PICO_WGRAD_GROUP (2 = pairs .. 8) when set; else 8 for a weight
+    whose gradient accumulates into DataParallelBucket's fp32 main_grad, 4 otherwise. C2 step, same box, 3
+    alternating rounds (profiles/r05_ab_wgrad_group.jsonl): 4 vs 2 — 823.7 -> 818.9 ms, under DataParallelBucket
+    854.3 -> 837.3 ms (half the fp32 main_grad read-modify-writes); 8 vs 4 under DataParallelBucket (RCCL W = 1,
+    2 alternating rounds, profiles/r06_ab_dp_group.jsonl): 844.5 / 844.3 -> 840.8 / 840.8 ms (plain step 826.8 /
+    828.0), group buffers 28.9 -> 57.8 GB; without main_grad 8 measured neutral (round 5)."""
+    env = os.getenv("PICO_WGRAD_GROUP")
+    if env is None:
+        mg = getattr(weight, "main_grad", None)
+        return 8 if mg is not None and mg.dtype == torch.float32 else 4
+    g = int(env)
     if g < 2 or g > 8:
         raise ValueError(f"PICO_WGRAD_GROUP={g}: 2..8 micro-batches per weight-gradient GEMM")
     return g
@@ -117,7 +124,7 @@ class PairBuf:
 def buf(weight, N, K, T, dtype, device):
     """The pair buffers of `weight` (created on first use; recreated if the shape changed)."""
     b = _get(weight)
-    G = group_size()
+    G = group_size(weight)
     if b is None or (b.N, b.K, b.T, b.G) != (N, K, T, G) or b.dy.dtype != dtype or b.dy.device != device:
         if b is not None and b.pending is not None:
             raise RuntimeError("paired weight gradients (wgrad_pair) need the micro-batches of a pair to have one "
