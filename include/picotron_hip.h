@@ -93,7 +93,8 @@ int pico_prof_collect(int kernel_id, double* total_ms, int64_t* launches);
  * the environment. */
 #define PICO_SEL_AUTO (-1)
 enum {
-  PICO_SEL_ATTN_KVP = 0,    /* PICO_ATTN_KVP: D=64 dK/dV kernel, 1 = 64-row attn_bwd_kvp_kernel, 0 = 32-row kernel */
+  PICO_SEL_ATTN_KVP = 0,    /* PICO_ATTN_KVP: dK/dV kernel, 1 = 64-row (attn_bwd_kvp_kernel at D=64,
+                               attn_bwd_kvp128_kernel at D=128), 0 = 32-row kernel */
   PICO_SEL_KVP_WAVES = 1,   /* PICO_KVP_WAVES: waves per attn_bwd_kvp_kernel workgroup, 4 or 8 */
   PICO_SEL_ATTN_GROUPS = 2, /* PICO_ATTN_GROUPS: one-round block groups of the causal dK/dV grid, 1 on / 0 off */
   PICO_SEL_ATTN_FWD = 3,    /* PICO_ATTN_FWD: 1 = the persistent 64-row-per-wave forward (opt-in, measured slower) */
