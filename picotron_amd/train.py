@@ -110,6 +110,21 @@ def train_step(model, data_loader, device, graphs=None, sync_loss=True):
         if grouped and not sync:
             pending.append((input_ids, target_ids))
             continue
+        if grouped and sync and pending and getattr(graphs, "tail_overlap", False) and tail_overlap_enabled():
+            # the syncing micro-batch's forward runs beside the graph's last backward (bwd n - 2 on a side stream);
+            # its backward, whose hooks launch the RCCL all-reduces, stays eager after both
+            def fwd_sync(x=input_ids, y=target_ids, j=i):
+                model.require_backward_grad_sync = True
+                with (WP.micro_batch(j, n) if pair else contextlib.nullcontext()):
+                    return _forward_loss(model, x, y, n)
+            model.require_backward_grad_sync = False
+            loss, folded = graphs.run(pending, between=fwd_sync)
+            pending.clear()
+            model.require_backward_grad_sync = True
+            with (WP.micro_batch(i, n) if pair else contextlib.nullcontext()):
+                loss.backward()
+            losses.append(loss.detach())
+            continue
         run_pending()
         if requires_grad_sync:
             model.require_backward_grad_sync = sync
@@ -206,6 +221,7 @@ class PipelinedMicroBatchGraph:
     micro-batch; `train_step` hands it the step's non-syncing micro-batches together (`run`)."""
 
     grouped = True
+    tail_overlap = True  # run(batches, between=...): the split head / tail capture
 
     def __init__(self, model, grad_acc_steps, zero_grads):
         self.model = model
@@ -215,16 +231,32 @@ class PipelinedMicroBatchGraph:
         self.loss_acc = None
         self.streams = None
         self.pair_latched = None
+        self.tail_stream = None  # the split capture's tail replays here (run(between=...))
+        self._tail_state = None
 
     @property
     def graph(self):
         return next(iter(self.graphs.values()))[0] if self.graphs else None
 
-    def _body(self, inp, tgt):
+    def _body(self, inp, tgt, part="all"):
+        """Issue the pipeline: part "all"; or "head" (everything but the last backward) then "tail" (that backward),
+        captured as two graphs so that the syncing micro-batch's eager forward can run beside the tail (run)."""
         from . import ops
         model, n, acc = self.model, self.n, self.loss_acc
-        WP.begin_step()  # each run of the body (eager warm-up, capture) issues the step's micro-batches from 0
         cur = torch.cuda.current_stream()
+        if part == "tail":
+            st = self._tail_state
+            self._tail_state = None
+            k = inp.shape[0]
+            s = (cur, self.streams[1])[(k - 1) % 2]
+            if s is not cur:
+                s.wait_stream(cur)
+            st["bwd_done"] = None  # the head ran to its end before the tail starts (stream order)
+            self._issue(k, k, model, n, acc, (cur, self.streams[1]), inp, tgt, st)
+            if s is not cur:
+                cur.wait_stream(s)
+            return
+        WP.begin_step()  # each run of the body (eager warm-up, capture) issues the step's micro-batches from 0
         # no dgrad / wgrad side-stream pairs (ops.dgrad_wgrad) inside the pipeline: a fork from slot 1's stream
         # crashes the capture (ops.no_side_streams), and on slot 0 alone they measured slower (C2 154.2 -> 152.2 K
         # tokens/s, profiles/r04_ab_pipeline_side0.jsonl): the other micro-batch already fills the chip.
@@ -235,39 +267,45 @@ class PipelinedMicroBatchGraph:
         streams[1].wait_stream(cur)
         # (a third stream for the grouped weight-gradient GEMMs, waits routed through the capture stream, measured
         # 4.7 % slower: DESIGN.md §4e)
-        self._slots(model, n, acc, streams, inp, tgt)
-        cur.wait_stream(streams[1])
-
-    def _slots(self, model, n, acc, streams, inp, tgt):
-        from . import ops
         k = inp.shape[0]
-        losses = [None] * k
-        bwd_done = fwd_done = None
+        st = {"losses": [None] * k, "bwd_done": None, "fwd_done": None}
         # (layer-ordered backwards -- backward i entering each layer after backward i - 1 left it -- measured
         # bit-identical and step-neutral in round 5, and removed)
-        for i in range(k + 1):
-            if i >= 1:  # backward of micro-batch i - 1 (on its forward's stream), after backward i - 2
-                st = streams[(i - 1) % 2]
-                with torch.cuda.stream(st), ops.no_side_streams(), WP.micro_batch(i - 1, n):
-                    if bwd_done is not None:
-                        st.wait_event(bwd_done)
-                    loss, folded = losses[i - 1]
-                    loss.backward()
-                    if not folded:
-                        acc += loss.detach()
-                    bwd_done = torch.cuda.Event()
-                    bwd_done.record(st)
-                losses[i - 1] = None
-            if i < k:  # forward of micro-batch i, after forward i - 1
-                st = streams[i % 2]
-                with torch.cuda.stream(st), ops.no_side_streams(), WP.micro_batch(i, n):
-                    if fwd_done is not None:
-                        st.wait_event(fwd_done)
-                    losses[i] = _forward_loss(model, inp[i], tgt[i], n, acc)
-                    fwd_done = torch.cuda.Event()
-                    fwd_done.record(st)
+        for i in range(k + 1 if part == "all" else k):
+            self._issue(i, k, model, n, acc, streams, inp, tgt, st)
+        cur.wait_stream(streams[1])
+        if part == "head":
+            self._tail_state = st
 
-    def _capture(self, batches):
+    def _issue(self, i, k, model, n, acc, streams, inp, tgt, st):
+        """Pipeline step i: the backward of micro-batch i - 1 (on its forward's stream, after backward i - 2), then
+        the forward of micro-batch i (after forward i - 1)."""
+        from . import ops
+        losses = st["losses"]
+        if i >= 1:
+            s = streams[(i - 1) % 2]
+            with torch.cuda.stream(s), ops.no_side_streams(), WP.micro_batch(i - 1, n):
+                if st["bwd_done"] is not None:
+                    s.wait_event(st["bwd_done"])
+                loss, folded = losses[i - 1]
+                loss.backward()
+                if not folded:
+                    acc += loss.detach()
+                ev = torch.cuda.Event()
+                ev.record(s)
+                st["bwd_done"] = ev
+            losses[i - 1] = None
+        if i < k:
+            s = streams[i % 2]
+            with torch.cuda.stream(s), ops.no_side_streams(), WP.micro_batch(i, n):
+                if st["fwd_done"] is not None:
+                    s.wait_event(st["fwd_done"])
+                losses[i] = _forward_loss(model, inp[i], tgt[i], n, acc)
+                ev = torch.cuda.Event()
+                ev.record(s)
+                st["fwd_done"] = ev
+
+    def _capture(self, batches, split=False):
         dev = batches[0][0].device
         if self.streams is None:
             self.streams = (None, torch.cuda.Stream(device=dev))  # slot 0: the caller's (capture) stream
@@ -282,20 +320,65 @@ class PipelinedMicroBatchGraph:
                 self._body(inp, tgt)
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            self._body(inp, tgt)
+        if split:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._body(inp, tgt, "head")
+            head_state = WP.pending_state()
+            g2 = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g2, pool=g.pool()):
+                self._body(inp, tgt, "tail")
+            tail_state = WP.pending_state()
+        else:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._body(inp, tgt)
         torch.cuda.synchronize()
         self.zero_grads()
         self.loss_acc.zero_()
         # a first half the graph's last micro-batch leaves deferred (wgrad_pair) for the eager one after it: the
         # replay runs no Python, so run() re-announces it after every replay
-        self.graphs[len(batches)] = (g, inp, tgt, WP.pending_state())
+        if split:
+            self.graphs[(len(batches), True)] = (g, inp, tgt, head_state, g2, tail_state)
+        else:
+            self.graphs[len(batches)] = (g, inp, tgt, WP.pending_state())
         self.pair_latched = WP.enabled()  # the pairing decisions are baked into the graph
 
-    def run(self, batches):
+    def run(self, batches, between=None):
+        """Replay the graph of these micro-batches. between (callable, optional): issued on the caller's stream while
+        the graph's last backward replays on a side stream (the split capture: head graph, then the tail beside
+        `between`); its return value is returned. The tail's effects are complete on the caller's stream on return."""
         from . import ops
         ops.refresh_weight_transposes()  # dgrad W^T copies are graph inputs: bring them up to date
+        if between is not None:
+            key = (len(batches), True)
+            if key not in self.graphs:
+                self._capture(batches, split=True)
+            if WP.enabled() != self.pair_latched:
+                raise RuntimeError("PipelinedMicroBatchGraph: PICO_WGRAD_PAIR changed after the graph was captured (its "
+                                   "wgrad pairing is fixed at capture); build a new graph")
+            g, inp, tgt, head_state, g2, tail_state = self.graphs[key]
+            for j, (x, y) in enumerate(batches):
+                inp[j].copy_(x)
+                tgt[j].copy_(y)
+            g.replay()
+            WP.restore_pending(head_state)
+            cur = torch.cuda.current_stream()
+            if self.tail_stream is None:
+                self.tail_stream = torch.cuda.Stream(device=inp.device)
+            self.tail_stream.wait_stream(cur)
+            with torch.cuda.stream(self.tail_stream):
+                g2.replay()
+            out = between()
+            cur.wait_stream(self.tail_stream)
+            # the tail's group-state changes (deferrals of the last backward), on top of what `between` changed
+            for b, v in tail_state.items():
+                if head_state.get(b) != v:
+                    b.pending = v
+            for b in head_state:
+                if b not in tail_state:
+                    b.pending = None
+            return out
         if len(batches) not in self.graphs:
             self._capture(batches)
         if WP.enabled() != self.pair_latched:
@@ -314,6 +397,12 @@ class PipelinedMicroBatchGraph:
         out = self.loss_acc.clone()
         self.loss_acc.zero_()
         return out
+
+
+def tail_overlap_enabled():
+    """PICO_DP_TAIL_OVERLAP (default 1): under a DP wrapper the syncing micro-batch's forward runs beside the
+    pipelined graph's last backward (the graph captured as head + tail), only its backward eager after both."""
+    return os.getenv("PICO_DP_TAIL_OVERLAP", "1") != "0"
 
 
 def pipelined_enabled():

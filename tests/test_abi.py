@@ -237,6 +237,54 @@ def test_train_step_groups_non_syncing_micro_batches():
     assert m.log == [("group", False, firsts[:3]), ("eager", True, firsts[3])], m.log
 
 
+def test_train_step_syncing_forward_beside_graph_tail():
+    """train_step with a grouped graph object that takes `between` (PipelinedMicroBatchGraph.tail_overlap): the
+    non-syncing micro-batches replay with the DP sync flag off, the syncing micro-batch's forward is issued through
+    `between` (inside the replay, beside the graph's last backward) with the flag on, and its backward runs after
+    the replay returns (host logic; a CPU stand-in model and graph object)."""
+    from picotron_amd.data import SyntheticDataLoader
+    from picotron_amd.train import train_step
+
+    class Tiny(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.emb = torch.nn.Embedding(64, 8)
+            self.out = torch.nn.Linear(8, 64, bias=False)
+            self.require_backward_grad_sync = True
+            self.log = []
+            self.out.weight.register_hook(lambda g: self.log.append(("backward", self.require_backward_grad_sync)))
+
+        def forward(self, input_ids):
+            self.log.append(("eager", self.require_backward_grad_sync, input_ids[0, 0].item()))
+            return self.out(self.emb(input_ids))
+
+    class Grouped:
+        grouped = True
+        tail_overlap = True
+
+        def __init__(self, model):
+            self.model = model
+
+        def run(self, batches, between=None):
+            self.model.log.append(("group", self.model.require_backward_grad_sync,
+                                   [b[0][0, 0].item() for b in batches]))
+            out = between() if between is not None else None
+            self.model.log.append(("tail done",))
+            return out
+
+        def take_loss(self):
+            return torch.zeros(())
+
+    m = Tiny()
+    loader = SyntheticDataLoader(2, 16, 4, 64, seed=3, num_batches=4)
+    firsts = [next(loader)["input_ids"][0, 0].item() for _ in range(4)]
+    loader = SyntheticDataLoader(2, 16, 4, 64, seed=3, num_batches=4)
+    loss = train_step(m, loader, "cpu", graphs=Grouped(m))
+    assert m.log == [("group", False, firsts[:3]), ("eager", True, firsts[3]), ("tail done",), ("backward", True)], \
+        m.log
+    assert loss > 0
+
+
 def test_wgrad_pair_plan(monkeypatch):
     """wgrad_pair's decisions (host logic, CPU tensors): the first micro-batch of a pair whose operands sit in the
     pair buffers defers, the second runs one GEMM over both halves; no partner (odd grad_acc) or operands elsewhere
