@@ -1385,7 +1385,8 @@ int kvp_waves(const pico_attn_args* a) {
 //     M1(A) | A's then B's Q / dO operands,  M1(B) | V(A) + A's transposed reads,  M2(A) | V(B) + B's reads,
 //     M2(B) | the DMA of tile t + 2
 // 16 MFMAs per phase (64 per tile: at D = 128 the tile is MFMA-bound, ~130 VALU against 2,048 matrix cycles), one
-// wave per SIMD (the whole register file; one 99-KiB workgroup per CU). The 32-row kernel it replaces runs each
+// wave per SIMD (the whole register file: dK / dV and K / V in AGPRs, the S / dP pipeline in VGPRs; one 99-KiB
+// workgroup per CU). The 32-row kernel it replaces runs each
 // 32-row tile as one dependency chain (S / dP -> softmax -> dV / dK) at one wave per SIMD: 0.22 MFMA busy at C4.
 // Operands are read two slots ahead of their MFMA; the schedule is fenced per slot (sched_barrier).
 constexpr int QT2 = 64;  // query rows per ring tile (the D = 64 TU defines it with attn_bwd_kvp_kernel)
@@ -1404,6 +1405,14 @@ struct KV2Cfg {
 // byte offset of 16-byte chunk ch (0..15) of row `row` in a [64][128 x bf16] image of 8-row x 32-column subtiles of
 // 512 B (cdna_hip_programming.md T11 image (a)): the row reads of a k-step parity and the transposed reads of a row
 // parity share one base register each (every other offset an immediate), both conflict-free
+// dV / dK accumulation into AGPR-resident accumulators: the compiler sees an opaque instruction, so the asm carries
+// what its hazard recognizer would add (s_nop 1: VALU write -> MFMA read of the packed P / dS operand, 2 wait
+// states); the accumulators are AGPR-class from their zero-initialisation (no copies at the loop edge) and read
+// only after the drain before the epilogue
+PICO_DEV void mfma32_acc(f32x16& acc, const bf16x8& x, const bf16x8& y) {
+  asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(x), "v"(y));
+}
+
 PICO_DEV int kv2_off(int row, int ch) {
   return 2048 * (row >> 3) + 512 * (ch >> 2) + 64 * (row & 7) + 16 * ((ch & 3) ^ ((row >> 2) & 3));
 }
@@ -1560,12 +1569,15 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kvp128_kernel(const pico_attn
       }
     }
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) asm volatile("" : "+v"(kf[ks]), "+v"(vf[ks]));
+    for (int ks = 0; ks < KS; ++ks) {
+      asm volatile("" : "+a"(kf[ks]), "+a"(vf[ks]));  // resident in AGPRs: the MFMAs take their B operand there
+    }
     f32x16 dk[DT], dv[DT];
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) {
       dk[dt] = (f32x16)0.f;
       dv[dt] = (f32x16)0.f;
+      asm volatile("" : "+a"(dk[dt]), "+a"(dv[dt]));
     }
     // row-read bases by k-step parity (k-step ks adds 512 (ks >> 1), half X 8192), transposed-read bases of rows
     // 4 hh + q and + 8 (tile dt adds 512 dt, 16-row step st 4096 st, half X 8192)
@@ -1695,8 +1707,8 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kvp128_kernel(const pico_attn
         static_for<2 * KS>([&](auto k_) {
           constexpr int k = decltype(k_)::value;
           constexpr int st = k / (2 * DT), dt = (k / 2) % DT;
-          if constexpr ((k & 1) == 0) dv[dt] = mfma32(toA[st][dt], pA[st], dv[dt]);
-          else dk[dt] = mfma32(tqA[st][dt], sAp[st], dk[dt]);
+          if constexpr ((k & 1) == 0) mfma32_acc(dv[dt], toA[st][dt], pA[st]);
+          else mfma32_acc(dk[dt], tqA[st][dt], sAp[st]);
           if constexpr ((k & 1) == 0) vpair(sB, dpB, k / 2, pwB[k / 2], swB[k / 2]);
           rd_tr(toB, tqB, 1, k);
           KV2_SLOT();
@@ -1709,8 +1721,8 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kvp128_kernel(const pico_attn
         static_for<2 * KS>([&](auto k_) {
           constexpr int k = decltype(k_)::value;
           constexpr int st = k / (2 * DT), dt = (k / 2) % DT;
-          if constexpr ((k & 1) == 0) dv[dt] = mfma32(toB[st][dt], pB[st], dv[dt]);
-          else dk[dt] = mfma32(tqB[st][dt], sBp[st], dk[dt]);
+          if constexpr ((k & 1) == 0) mfma32_acc(dv[dt], toB[st][dt], pB[st]);
+          else mfma32_acc(dk[dt], tqB[st][dt], sBp[st]);
           if constexpr ((k & 1) == 1) {  // image pieces 0..7 in the odd slots (measured: 2, 4 or all 8 of them
             if (dma_next) issue_piece(dslot, nxt, k / 2);  // in M2(A)'s slots instead is 0-3 % slower)
           } else if constexpr (k == 0) {  // the LSE / delta piece
@@ -1724,6 +1736,10 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kvp128_kernel(const pico_attn
       q0cur = q0cur + QT2 >= qend ? qstart : q0cur + QT2;
     }
     }
+    // the last accumulations complete (32x32 MFMA write -> read: up to 18 wait states) before the epilogue reads them
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7"
+                 : "+a"(dk[0]), "+a"(dk[1]), "+a"(dk[2]), "+a"(dk[3]), "+a"(dv[0]), "+a"(dv[1]), "+a"(dv[2]),
+                   "+a"(dv[3]));
 #if PICO_KVP_STAMP
     const unsigned long long tep = __builtin_amdgcn_s_memtime();
 #endif
