@@ -1439,6 +1439,9 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kvp128_kernel(const pico_attn
 #define KV2_ST(i)
 #endif
   constexpr int KS = C::KS, DT = C::DT, PPW = C::PPW, NW = 4, KB = 32 * NW;
+  // M1 operands are read RD slots ahead of their MFMA (3 vs 2: 0.7-1.4 % less time at C4 / non-causal / GQA-4 over
+  // 2 x 2 rounds, profiles/r06_kvp128_rd/; 4 no better)
+  constexpr int RD = 3;
   static_assert(PPW == 8 && 2 * C::NQP == PPW * NW, "8 image pieces per wave: the odd slots of M2(B)");
   __shared__ __attribute__((aligned(16))) char smem[C::NBUF * C::SLOT];
 
@@ -1672,16 +1675,15 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kvp128_kernel(const pico_attn
       // ---- M1(A): S_A (k < KS), dP_A (k >= KS); operands two slots ahead; B's first operands + initial values ----
       f32x16 sA = init_rows(lsd, 0, 0), dpA = init_rows(lsd, 0, 1);
       if (diag) mask_rows(sA, q0cur);
-      rd_op(opA, 0, 0);
-      rd_op(opA, 0, 1);
+      static_for<RD>([&](auto k_) { rd_op(opA, 0, decltype(k_)::value); });
       f32x16 sB, dpB;
       KV2_SLOT();
       static_for<2 * KS>([&](auto k_) {
         constexpr int k = decltype(k_)::value;
         if constexpr (k < KS) sA = mfma32(opA[k], kf[k], sA);
         else dpA = mfma32(opA[k], vf[k - KS], dpA);
-        if constexpr (k + 2 < 2 * KS) rd_op(opA, 0, k + 2);
-        else rd_op(opB, 1, k + 2 - 2 * KS);
+        if constexpr (k + RD < 2 * KS) rd_op(opA, 0, k + RD);
+        else rd_op(opB, 1, k + RD - 2 * KS);
         if constexpr (k == 4) sB = init_rows(lsd, 1, 0);
         if constexpr (k == 6) dpB = init_rows(lsd, 1, 1);
         if constexpr (k == 8) {
@@ -1695,7 +1697,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kvp128_kernel(const pico_attn
         constexpr int k = decltype(k_)::value;
         if constexpr (k < KS) sB = mfma32(opB[k], kf[k], sB);
         else dpB = mfma32(opB[k], vf[k - KS], dpB);
-        if constexpr (k + 2 < 2 * KS) rd_op(opB, 1, k + 2);
+        if constexpr (k + RD < 2 * KS) rd_op(opB, 1, k + RD);
         if constexpr ((k & 1) == 0) vpair(sA, dpA, k / 2, pwA[k / 2], swA[k / 2]);
         rd_tr(toA, tqA, 0, k);
         KV2_SLOT();
