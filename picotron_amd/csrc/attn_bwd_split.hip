@@ -155,6 +155,19 @@ PICO_DEV void tr_offsets(int lane, unsigned (&tro)[D / 32][2]) {
   }
 }
 
+// Accumulation into AGPR-resident accumulators (attn_bwd_kvp128_kernel: the VGPR-form build keeps every builtin MFMA's
+// accumulator in VGPRs, which the wave cannot hold beside its S / dP pipeline; the same form in the D = 128 dQ
+// kernel, two waves per SIMD, measured slower: C4 41.0 -> 44.8 us, profiles/r06_dq128_agpr/): the compiler sees an opaque
+// instruction, so the asm carries what its hazard recognizer would add (s_nop 1: VALU write -> MFMA read of the
+// packed operand, 2 wait states); the accumulators are AGPR-class from their zero-initialisation (no copies at the
+// loop edge) and are read only after a drain (acc_drain: the last MFMA's write before any VALU read)
+PICO_DEV void mfma32_acc(f32x16& acc, const bf16x8& x, const bf16x8& y) {
+  asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(x), "v"(y));
+}
+PICO_DEV void acc_drain4(f32x16 (&v)[4]) {
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" : "+a"(v[0]), "+a"(v[1]), "+a"(v[2]), "+a"(v[3]));
+}
+
 // ------------------------------------------------------------------------------------------------
 // dQ kernel (query-major)
 // ------------------------------------------------------------------------------------------------
@@ -1405,14 +1418,6 @@ struct KV2Cfg {
 // byte offset of 16-byte chunk ch (0..15) of row `row` in a [64][128 x bf16] image of 8-row x 32-column subtiles of
 // 512 B (cdna_hip_programming.md T11 image (a)): the row reads of a k-step parity and the transposed reads of a row
 // parity share one base register each (every other offset an immediate), both conflict-free
-// dV / dK accumulation into AGPR-resident accumulators: the compiler sees an opaque instruction, so the asm carries
-// what its hazard recognizer would add (s_nop 1: VALU write -> MFMA read of the packed P / dS operand, 2 wait
-// states); the accumulators are AGPR-class from their zero-initialisation (no copies at the loop edge) and read
-// only after the drain before the epilogue
-PICO_DEV void mfma32_acc(f32x16& acc, const bf16x8& x, const bf16x8& y) {
-  asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(x), "v"(y));
-}
-
 PICO_DEV int kv2_off(int row, int ch) {
   return 2048 * (row >> 3) + 512 * (ch >> 2) + 64 * (row & 7) + 16 * ((ch & 3) ^ ((row >> 2) & 3));
 }
@@ -1739,9 +1744,8 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kvp128_kernel(const pico_attn
     }
     }
     // the last accumulations complete (32x32 MFMA write -> read: up to 18 wait states) before the epilogue reads them
-    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7"
-                 : "+a"(dk[0]), "+a"(dk[1]), "+a"(dk[2]), "+a"(dk[3]), "+a"(dv[0]), "+a"(dv[1]), "+a"(dv[2]),
-                   "+a"(dv[3]));
+    acc_drain4(dk);
+    acc_drain4(dv);
 #if PICO_KVP_STAMP
     const unsigned long long tep = __builtin_amdgcn_s_memtime();
 #endif
