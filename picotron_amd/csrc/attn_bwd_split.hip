@@ -1408,7 +1408,8 @@ struct KV2Cfg {
   static constexpr int QIMG = QT2 * 256;         // one Q (or dO) 64-row image (kv2_off), 16 KiB
   static constexpr int LSD = 1024;               // -LSE/scale [64] | -delta [64] (+ 512 B the DMA piece repeats)
   static constexpr int SLOT = 2 * QIMG + LSD;    // 33 KiB
-  static constexpr int NBUF = 3, PD = NBUF - 1;  // 99 KiB per workgroup, prefetch distance 2
+  // 99 KiB per workgroup, prefetch distance 2 (a 4-deep ring measured 1-5 % slower)
+  static constexpr int NBUF = 3, PD = NBUF - 1;
   static constexpr int NQP = QIMG / 1024;        // 16 pieces per image
   static constexpr int PPW = 2 * NQP / 4;        // 8 image pieces per wave per tile (+ wave 0's LSE / delta piece)
 };
@@ -1643,7 +1644,12 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kvp128_kernel(const pico_attn
       ph[7] += 1;
 #endif
       if (t > 0) {
-        if (t + 1 < ntiles) {  // this wave's pieces of tile t landed; tile t + 1's stay in flight
+        // this wave's pieces of tile t landed; those of the younger tiles already issued stay in flight
+        const int younger = min(C::PD - 1, ntiles - 1 - t);
+        if (younger >= 2 && C::PD >= 3) {
+          if (wave == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (PPW + 1)) : "memory");
+          else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PPW) : "memory");
+        } else if (younger >= 1) {
           if (wave == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW + 1) : "memory");
           else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");
         } else {
