@@ -34,6 +34,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--configs", default="c2,d128")
+    ap.add_argument("--strided", action="store_true",
+                    help="q / k / v as strided views of one [B, S, (Hq + 2 Hkv) D] buffer (the training step's layout)")
     args = ap.parse_args()
     from picotron_amd import _lib as L
     from picotron_amd import ops
@@ -41,9 +43,13 @@ def main():
     for name in args.configs.split(","):
         B, S, Hq, Hkv, D, causal = CONFIGS[name]
         torch.manual_seed(0)
-        q = torch.randn(B, S, Hq, D, dtype=torch.bfloat16, device="cuda")
-        k = torch.randn(B, S, Hkv, D, dtype=torch.bfloat16, device="cuda")
-        v = torch.randn(B, S, Hkv, D, dtype=torch.bfloat16, device="cuda")
+        if args.strided:
+            qkv = torch.randn(B, S, Hq + 2 * Hkv, D, dtype=torch.bfloat16, device="cuda")
+            q, k, v = qkv.split([Hq, Hkv, Hkv], dim=2)
+        else:
+            q = torch.randn(B, S, Hq, D, dtype=torch.bfloat16, device="cuda")
+            k = torch.randn(B, S, Hkv, D, dtype=torch.bfloat16, device="cuda")
+            v = torch.randn(B, S, Hkv, D, dtype=torch.bfloat16, device="cuda")
         do = torch.randn(B, S, Hq, D, dtype=torch.bfloat16, device="cuda")
         sc = 1 / math.sqrt(D)
         for _ in range(3):
@@ -59,7 +65,7 @@ def main():
             ops.attention_block_bwd(do, q, k, v, o, lse, sc, causal)
         torch.cuda.synchronize()
         fl = 4.0 * B * Hq * S * S * D * (0.5 if causal else 1.0)
-        res = {"config": name, "B": B, "S": S, "Hq": Hq, "Hkv": Hkv, "D": D, "causal": causal}
+        res = {"config": name, "strided": args.strided, "B": B, "S": S, "Hq": Hq, "Hkv": Hkv, "D": D, "causal": causal}
         # wall time of the whole backward call on the caller's stream (kernel timers off): the dQ and dK/dV
         # kernels plus the launch gaps between them
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -2,7 +2,8 @@
 per workgroup s_memrealtime (100 MHz) at entry, loop start, loop end, stores drained. Prints the kernel span,
 mean prologue / loop / epilogue per workgroup, the loop share of the summed workgroup time, the mean number of
 workgroups resident over the span and the loop time per tile by query block.
-PICO_LIB_PATH=picotron_amd/lib/variants/fwdstamp.so python scripts/fwd_wgstamps.py [--full]"""
+PICO_LIB_PATH=picotron_amd/lib/variants/fwdstamp.so python scripts/fwd_wgstamps.py [--full] [--shape B,S,H,D]
+(--shape 4,1024,16,128: C4's per-rank D = 128 forward)"""
 import ctypes
 import json
 import math
@@ -20,6 +21,8 @@ from picotron_amd import ops  # noqa: E402
 def main():
     causal = "--full" not in sys.argv
     B, S, H, D = 4, 1024, 32, 64
+    if "--shape" in sys.argv:
+        B, S, H, D = (int(x) for x in sys.argv[sys.argv.index("--shape") + 1].split(","))
     torch.manual_seed(0)
     q, k, v = [torch.randn(B, S, H, D, device="cuda", dtype=torch.bfloat16) for _ in range(3)]
     o = torch.empty_like(q)
@@ -49,7 +52,7 @@ def main():
     mb = (nmb - 1 - lin // nbh) if causal else lin // nbh
     tiles = 2 * (mb + 1) if causal else np.full(nwg, S // 64)
     per_tile = {int(m): round(float((loop[mb == m] / tiles[mb == m]).mean()), 3) for m in range(nmb)}
-    print(json.dumps({"causal": causal, "workgroups": int(nwg), "span_us": round(span, 2),
+    print(json.dumps({"shape": [B, S, H, D], "causal": causal, "workgroups": int(nwg), "span_us": round(span, 2),
                       "prologue_us": round(pro.mean(), 2), "loop_us": round(loop.mean(), 2),
                       "epilogue_us": round(epi.mean(), 2), "loop_share_of_wg_time": round(loop.sum() / life.sum(), 3),
                       "mean_resident": round(float(np.mean(resident)), 1), "resident_profile": resident[::10],
