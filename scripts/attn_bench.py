@@ -36,6 +36,8 @@ def main():
     ap.add_argument("--configs", default="c2,d128")
     ap.add_argument("--strided", action="store_true",
                     help="q / k / v as strided views of one [B, S, (Hq + 2 Hkv) D] buffer (the training step's layout)")
+    ap.add_argument("--cold", action="store_true",
+                    help="overwrite a 1-GiB buffer before every iteration (the inputs leave L2 and the Infinity Cache)")
     args = ap.parse_args()
     from picotron_amd import _lib as L
     from picotron_amd import ops
@@ -60,12 +62,17 @@ def main():
                L.K_ATTN_BWD_KV]
         for i in ids:
             L.prof_enable(i, args.iters + 4)
+        flush = torch.empty(1 << 29, dtype=torch.bfloat16, device="cuda") if args.cold else None
         for _ in range(args.iters):
+            if flush is not None:
+                flush.fill_(1.0)
             o, lse = ops.attention_block_fwd(q, k, v, sc, causal)
+            if flush is not None:
+                flush.fill_(2.0)
             ops.attention_block_bwd(do, q, k, v, o, lse, sc, causal)
         torch.cuda.synchronize()
         fl = 4.0 * B * Hq * S * S * D * (0.5 if causal else 1.0)
-        res = {"config": name, "strided": args.strided, "B": B, "S": S, "Hq": Hq, "Hkv": Hkv, "D": D, "causal": causal}
+        res = {"config": name, "strided": args.strided, "cold": args.cold, "B": B, "S": S, "Hq": Hq, "Hkv": Hkv, "D": D, "causal": causal}
         # wall time of the whole backward call on the caller's stream (kernel timers off): the dQ and dK/dV
         # kernels plus the launch gaps between them
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
