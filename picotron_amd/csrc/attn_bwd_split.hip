@@ -2029,8 +2029,7 @@ int pico_attn_bwd_split(const pico_attn_args* a, hipStream_t s) {
   return a->causal ? launch_split<64, true>(a, s) : launch_split<64, false>(a, s);
 }
 #else
-// head_dim 128: its own translation unit (built without -amdgpu-mfma-vgpr-form: the D = 128 dK / dV and dQ
-// accumulators need the AGPR half of the register file)
+// head_dim 128: its own translation unit (its own per-file build flags, picotron_amd/build.py FILE_FLAGS)
 int pico_attn_bwd_split_d128(const pico_attn_args* a, hipStream_t s) {
   return a->causal ? launch_split<128, true>(a, s) : launch_split<128, false>(a, s);
 }
